@@ -1,0 +1,164 @@
+/*
+ * pt.h -- C-ABI drop-in boundary of the MI355X path tracer (libpt.so).
+ *
+ * The reference has no C ABI: its boundary is the C++ scene API of namespace
+ * PathTrace plus the templates tracePixel<T>/traceRay<T>.
+ * Every entry point below replaces one reference interface, cited per line.
+ * Plain pointers and sizes only; no exceptions cross the ABI: functions return
+ * a status (PT_OK = 0, negative on error) or an id (>= 0, negative on error),
+ * and pt_last_error() describes the last failure on the calling thread.
+ *
+ * Ownership mirrors the reference: a scene owns every texture, material,
+ * object and image created in it; ids stay valid until pt_scene_destroy.
+ * Objects may be referenced by several parents (the reference would
+ * duplicate() them), materials are shared by reference as in the reference
+ * (`const Material *`, include/sphere.h:12).
+ *
+ * Threading: a pt_scene may be rendered from one thread at a time; distinct
+ * scenes are independent.  Rendering is synchronous unless pt_render_device
+ * is given a stream.
+ */
+#ifndef PT_PT_H
+#define PT_PT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_ERR_ARG (-1)      /* bad id / argument (reference: assert or UB)          */
+#define PT_ERR_MATH (-2)     /* singular matrix: std::domain_error, transform.h:353   */
+#define PT_ERR_IO (-3)       /* ImageLoadError / ImageStoreError, image.h:30-46       */
+#define PT_ERR_DEVICE (-4)   /* HIP runtime failure or no device                      */
+#define PT_ERR_COMPILE (-5)  /* device code generation / hiprtc failure               */
+
+typedef struct pt_scene pt_scene;
+typedef int32_t pt_id;
+
+/* ------------------------------------------------------------ lifetime -- */
+pt_scene *pt_scene_create(void);
+void pt_scene_destroy(pt_scene *s);
+const char *pt_last_error(void);
+const char *pt_version(void);
+
+/* ------------------------------------------------------------- images --- */
+/* Image(string fileName) for ".hdr"/".pic" (reference src/image.cpp:83-324). */
+pt_id pt_image_load_hdr(pt_scene *s, const char *path);
+/* MutableImage -> Image (include/image.h:110-211): rgba is h rows of w RGBA
+ * floats, row 0 = top; copied. */
+pt_id pt_image_from_rgba32f(pt_scene *s, const float *rgba, int w, int h);
+/* Decode a Radiance HDR file into caller memory (w*h*4 floats); pass
+ * rgba=NULL to query the size. */
+int pt_hdr_read(const char *path, float *rgba, int *w, int *h);
+
+/* ----------------------------------------------------------- textures --- */
+pt_id pt_tex_color(pt_scene *s, float r, float g, float b);              /* ColorTexture       texture.h:29-58  */
+pt_id pt_tex_image(pt_scene *s, pt_id image);                            /* ImageTexture       image_texture.h:9-33 */
+pt_id pt_tex_image_alpha(pt_scene *s, pt_id image);                      /* ImageAlphaTexture  image_texture.h:35-70 */
+pt_id pt_tex_skybox(pt_scene *s, pt_id top, pt_id bottom, pt_id left,    /* ImageSkyboxTexture image_texture.h:72-115 */
+                    pt_id right, pt_id front, pt_id back);
+pt_id pt_tex_skybox_alpha(pt_scene *s, pt_id top, pt_id bottom, pt_id left, /* ImageSkyboxAlphaTexture :117-181 */
+                          pt_id right, pt_id front, pt_id back);
+pt_id pt_tex_multiply(pt_scene *s, float r, float g, float b, pt_id t);  /* MultiplyTexture    filter_texture.h:36-56 */
+pt_id pt_tex_log(pt_scene *s, pt_id t);                                  /* LogTexture         filter_texture.h:58-82 */
+pt_id pt_tex_mirrorball(pt_scene *s, pt_id t);                           /* MirrorBallSkymapTexture transform_texture.h:33-59 */
+pt_id pt_tex_spherical(pt_scene *s, pt_id t);                            /* SphericalCoordinatesSkymapTexture :61-85 */
+pt_id pt_tex_transformed(pt_scene *s, const float m[12], pt_id t);      /* TransformedTexture texture.h:60-90 */
+pt_id pt_tex_coord(pt_scene *s);                                         /* test instrument: colour = coordinate */
+
+/* ---------------------------------------------------------- materials --- */
+/* Material(reflect, scatter_coefficient, emissive, transmit, ior,
+ * transmit_reflect_coefficient), include/material.h:18.  Pass -1 for a
+ * texture to get the reference default (1, 1, 0, 0, -, 0). */
+pt_id pt_material(pt_scene *s, pt_id reflect, pt_id scatter, pt_id emissive, pt_id transmit, float ior,
+                  pt_id transmit_reflect);
+
+/* ------------------------------------------------------------ objects --- */
+pt_id pt_sphere(pt_scene *s, float cx, float cy, float cz, float r, pt_id mat);   /* Sphere  sphere.h:12 */
+pt_id pt_plane(pt_scene *s, float nx, float ny, float nz, float d, pt_id mat);    /* Plane(n, d)   plane.h:12 */
+pt_id pt_plane_through(pt_scene *s, float nx, float ny, float nz,                 /* Plane(n, pos) plane.h:13 */
+                       float px, float py, float pz, pt_id mat);
+#define PT_CSG_UNION 0        /* Union        union.h:12        */
+#define PT_CSG_INTERSECTION 1 /* Intersection intersection.h:12 */
+#define PT_CSG_DIFFERENCE 2   /* Difference   difference.h:12   */
+pt_id pt_csg(pt_scene *s, int op, pt_id a, pt_id b);
+pt_id pt_transformed(pt_scene *s, const float m[12], pt_id child);             /* TransformedObject object.h:78 */
+int pt_set_root(pt_scene *s, pt_id obj);
+/* Load a whole scene from the plain-text scene format (oracle/scene_text.h
+ * documents it; pathtrace.scene.to_text writes it).  Replaces the current
+ * contents of s. */
+int pt_scene_from_text(pt_scene *s, const char *text);
+
+/* ---------------------------------------------------- matrix helpers --- */
+/* Float arithmetic of include/transform.h:207-421, m in constructor order
+ * x00 x10 x20 x30 x01 x11 x21 x31 x02 x12 x22 x32. */
+void pt_matrix_rotate(const float axis[3], double angle, float out[12]);
+int pt_matrix_inverse(const float m[12], float out[12]);                /* PT_ERR_MATH if singular */
+void pt_matrix_concat(const float a[12], const float b[12], float out[12]);
+
+/* ------------------------------------------------------------- render --- */
+#define PT_ORDER_GROUP64 0   /* fast path: leaf children summed in 64-wide pairwise groups */
+#define PT_ORDER_REFERENCE 1 /* bit-for-bit the reference's sequential child order          */
+
+typedef struct pt_render_params {
+    int width, height;             /* screenXResolution, screenYResolution                      */
+    int spp;                       /* sampleCount                                               */
+    int depth;                     /* rayDepth                                                  */
+    float screen_w, screen_h;      /* screenWidth, screenHeight                                 */
+    float screen_dist;             /* screenDistance                                            */
+    uint64_t seed;                 /* run seed of the per-(pixel, sample) engine (pt_engine.h)  */
+    int order;                     /* PT_ORDER_*                                                */
+    int device;                    /* HIP device ordinal                                        */
+    const int32_t *pixels;         /* optional host list of pixel indices (y*width+x) to render;
+                                      NULL = all pixels                                         */
+    int64_t npixels;               /* length of pixels                                          */
+    int64_t max_buffer_bytes;      /* per-sample staging budget (0 = 8 GiB)                     */
+} pt_render_params;
+
+typedef struct pt_render_stats {
+    double kernel_ms;              /* summed render-kernel time (HIP events)                    */
+    double reduce_ms;              /* summed reduce-kernel time                                 */
+    uint64_t launches;             /* render-kernel launches                                    */
+    uint64_t samples;              /* traceRay calls from tracePixel                            */
+    uint64_t queries;              /* root span queries (spine + leaf children)                 */
+    uint64_t leaf_queries;         /* of which wave-cooperative leaf children                   */
+    uint64_t attempts;             /* rejection attempts evaluated (64 per round)               */
+    uint64_t rounds;               /* attempt rounds                                            */
+    uint64_t sphere_tests, sphere_hits, plane_tests;
+} pt_render_stats;
+
+/* Synchronous: renders the frame into rgb_out (host memory), which receives,
+ * for each pixel of params->pixels (or of the whole frame, row-major), the
+ * mean radiance (r, g, b) exactly as tracePixel returns it (path-trace.h:187-201).
+ * Replaces the per-pixel tracePixel calls of RenderBlock::calcPixelColor
+ * (reference src/test.cpp:441-465). */
+int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_stats *stats);
+
+/* Device variant: writes W*H*3 floats into device memory fb (full frame,
+ * row-major; pixels not listed in params->pixels are left untouched) on the
+ * given hipStream_t (NULL = default stream) and returns once the work is
+ * enqueued... or completed when stats != NULL (stats need the timings). */
+int pt_render_device(pt_scene *s, const pt_render_params *p, float *fb, void *stream, pt_render_stats *stats);
+
+/* JIT-compile (or fetch from the code-object cache) the megakernel for this
+ * scene and depth without touching a GPU.  Used by build() to pre-populate the
+ * in-tree cache. */
+int pt_scene_compile(pt_scene *s, int depth);
+/* Key of the code object for this scene/depth (hex string, static storage). */
+const char *pt_scene_kernel_key(pt_scene *s, int depth);
+
+/* ------------------------------------------------------------- output --- */
+/* MutableImage::writeHDR (reference src/image.cpp:398-481), rgb = w*h*3 floats. */
+int pt_write_hdr(const char *path, const float *rgb, int w, int h);
+/* 24-bpp BGR bottom-up BMP as SDL_SaveBMP writes it, bytes
+ * clamp(floor(256*c/count), 0, 255) (reference src/test.cpp:1037-1059). */
+int pt_write_bmp(const char *path, const float *rgb, int w, int h, int count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

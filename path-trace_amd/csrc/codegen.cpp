@@ -1,0 +1,253 @@
+/*
+ * codegen.cpp -- flattens a scene graph into a device module: the CSG tree
+ * becomes a compile-time type over pt_device.h's node templates, every float
+ * the nodes and textures need goes into the parameter block P at a fixed
+ * offset, and the materials become switch dispatchers.  The reference's
+ * virtual calls (SpanIterator::init/next, Texture::getColor/getFloat) thus
+ * turn into straight-line, fully inlined code per scene.
+ */
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <sstream>
+
+#include "internal.h"
+
+namespace pt
+{
+
+namespace
+{
+
+struct Gen
+{
+    const SceneImpl &s;
+    std::vector<float> P;
+    std::map<int, int> mat_index;   /* scene material id -> compact index */
+    std::vector<int> mats;          /* compact index -> scene material id */
+    std::map<int, int> img_slot;    /* scene image id -> slot */
+    std::vector<int> images;
+    int prim = 0, spheres = 0, planes = 0;
+    int depth_guard = 0;
+
+    explicit Gen(const SceneImpl &sc) : s(sc) {}
+
+    int put(const float *v, int n)
+    {
+        int off = (int)P.size();
+        P.insert(P.end(), v, v + n);
+        return off;
+    }
+
+    int material(int id)
+    {
+        auto it = mat_index.find(id);
+        if (it != mat_index.end())
+            return it->second;
+        int k = (int)mats.size();
+        if (k >= 4096)
+            throw Error(PT_ERR_ARG, "too many materials (max 4096)");
+        mat_index[id] = k;
+        mats.push_back(id);
+        return k;
+    }
+
+    int slot(int img)
+    {
+        auto it = img_slot.find(img);
+        if (it != img_slot.end())
+            return it->second;
+        int k = (int)images.size();
+        img_slot[img] = k;
+        images.push_back(img);
+        return k;
+    }
+
+    std::string obj(int id)
+    {
+        if (++depth_guard > 10000)
+            throw Error(PT_ERR_ARG, "scene graph too deep");
+        const ObjRec &o = s.objects.at(id);
+        std::ostringstream t;
+        switch (o.kind) {
+        case ObjKind::Sphere: {
+            float v[4] = {o.f[0], o.f[1], o.f[2], o.f[3] * o.f[3]}; /* r_squared = r * r, sphere.cpp:10 */
+            int off = put(v, 4);
+            t << "Sph<" << prim++ << "," << off << "," << material(o.mat) << ">";
+            spheres++;
+            break;
+        }
+        case ObjKind::Plane: {
+            int off = put(o.f, 4);
+            t << "Pln<" << prim++ << "," << off << "," << material(o.mat) << ">";
+            planes++;
+            break;
+        }
+        case ObjKind::Union:
+        case ObjKind::Intersection:
+        case ObjKind::Difference: {
+            const char *n = o.kind == ObjKind::Union ? "Uni" : o.kind == ObjKind::Intersection ? "Isect" : "Diff";
+            std::string a = obj(o.a);
+            std::string b = obj(o.b);
+            t << n << "<" << a << "," << b << ">";
+            break;
+        }
+        case ObjKind::Xform: {
+            float inv[12];
+            mat_inverse(o.f, inv); /* TransformedSpanIterator: inv(invert(m)), object.h:49-51 */
+            int moff = put(o.f, 12);
+            int ioff = put(inv, 12);
+            t << "Xf<" << moff << "," << ioff << "," << obj(o.a) << ">";
+            break;
+        }
+        }
+        if (prim >= (1 << 17))
+            throw Error(PT_ERR_ARG, "too many primitives");
+        return t.str();
+    }
+
+    std::string tex(int id)
+    {
+        const TexRec &x = s.textures.at(id);
+        std::ostringstream t;
+        switch (x.kind) {
+        case TexKind::Color:
+            t << "TConst<" << put(x.f, 3) << ">";
+            break;
+        case TexKind::Coord:
+            t << "TCoord";
+            break;
+        case TexKind::Image:
+            t << "TImage<" << slot(x.img[0]) << ">";
+            break;
+        case TexKind::ImageAlpha:
+            t << "TImageAlpha<" << slot(x.img[0]) << ">";
+            break;
+        case TexKind::Skybox:
+        case TexKind::SkyboxAlpha:
+            t << (x.kind == TexKind::Skybox ? "TSkybox<" : "TSkyboxAlpha<");
+            for (int k = 0; k < 6; k++) t << (k ? "," : "") << slot(x.img[k]);
+            t << ">";
+            break;
+        case TexKind::Multiply: {
+            int off = put(x.f, 3);
+            t << "TMul<" << off << "," << tex(x.child) << ">";
+            break;
+        }
+        case TexKind::Log:
+            t << "TLog<" << tex(x.child) << ">";
+            break;
+        case TexKind::MirrorBall:
+            t << "TMirrorBall<" << tex(x.child) << ">";
+            break;
+        case TexKind::Spherical:
+            t << "TSpherical<" << tex(x.child) << ">";
+            break;
+        case TexKind::Xform: {
+            int off = put(x.f, 12);
+            t << "TXf<" << off << "," << tex(x.child) << ">";
+            break;
+        }
+        }
+        return t.str();
+    }
+};
+
+uint64_t fnv1a(const std::string &s, uint64_t h = 1469598103934665603ull)
+{
+    for (unsigned char c : s) {
+        h ^= c;
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+} // namespace
+
+Generated generate(const SceneImpl &s, int depth)
+{
+    if (s.root < 0)
+        throw Error(PT_ERR_ARG, "scene has no root object (pt_set_root)");
+    Gen g(s);
+    std::string root = g.obj(s.root);
+
+    /* material dispatchers; texture params are appended after geometry */
+    struct MatTypes
+    {
+        std::string refl, scat, emis, trans, trc;
+        bool emis_const;
+        int emis_off;
+    };
+    std::vector<MatTypes> mt;
+    for (size_t k = 0; k < g.mats.size(); k++) {
+        const MatRec &m = s.materials.at(g.mats[k]);
+        MatTypes t;
+        t.refl = g.tex(m.reflect);
+        t.scat = g.tex(m.scatter);
+        t.emis = g.tex(m.emissive);
+        t.trans = g.tex(m.transmit);
+        t.trc = g.tex(m.trc);
+        t.emis_const = s.textures.at(m.emissive).kind == TexKind::Color;
+        mt.push_back(t);
+    }
+    int ior_off = (int)g.P.size();
+    for (size_t k = 0; k < g.mats.size(); k++) g.P.push_back(s.materials.at(g.mats[k]).ior);
+    bool all_emis_const = true;
+    for (auto &t : mt) all_emis_const = all_emis_const && t.emis_const;
+    int emis_tab = -1;
+    if (all_emis_const) {
+        emis_tab = (int)g.P.size();
+        for (size_t k = 0; k < g.mats.size(); k++) {
+            const TexRec &e = s.textures.at(s.materials.at(g.mats[k]).emissive);
+            g.P.insert(g.P.end(), e.f, e.f + 3);
+        }
+    }
+
+    int maxd = 4;
+    while (maxd < depth) maxd *= 2;
+
+    std::ostringstream src;
+    src << device_library_source() << "\n";
+    src << "namespace ptgen {\nusing namespace ptd;\n";
+    src << "typedef " << root << " RootT;\n";
+    src << "struct Scene {\n  typedef RootT Root;\n";
+    auto dispatch = [&](const char *name, const char *ret, const char *fn, std::string MatTypes::*field) {
+        src << "  __device__ static __forceinline__ " << ret << " " << name
+            << "(int m, V3 p, const Env &e) {\n    switch (m) {\n";
+        for (size_t k = 0; k < mt.size(); k++)
+            src << "    case " << k << ": return " << mt[k].*field << "::" << fn << "(p, e);\n";
+        src << "    default: return " << (std::string(ret) == "V3" ? "mk(0, 0, 0)" : "0.0f") << ";\n    }\n  }\n";
+    };
+    if (all_emis_const) {
+        src << "  __device__ static __forceinline__ V3 emis(int m, V3, const Env &e) {\n"
+            << "    const float *t = e.P + " << emis_tab << " + 3 * m;\n    return mk(t[0], t[1], t[2]);\n  }\n";
+    } else {
+        dispatch("emis", "V3", "color", &MatTypes::emis);
+    }
+    dispatch("refl", "V3", "color", &MatTypes::refl);
+    dispatch("trans", "V3", "color", &MatTypes::trans);
+    dispatch("scat", "float", "value", &MatTypes::scat);
+    dispatch("trc", "float", "value", &MatTypes::trc);
+    src << "  __device__ static __forceinline__ float ior(int m, const Env &e) { return e.P[" << ior_off
+        << " + m]; }\n";
+    src << "};\n} // namespace ptgen\n";
+    src << "PT_DEFINE_KERNELS(ptgen::Scene, " << maxd << ")\n";
+
+    Generated out;
+    out.source = src.str();
+    out.params = std::move(g.P);
+    if (out.params.empty())
+        out.params.push_back(0.0f);
+    out.image_ids = g.images;
+    out.maxd = maxd;
+    out.n_prims = g.prim;
+    out.n_spheres = g.spheres;
+    out.n_planes = g.planes;
+    out.n_mats = (int)g.mats.size();
+    char key[40];
+    snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(out.source));
+    out.key = key;
+    return out;
+}
+
+} // namespace pt

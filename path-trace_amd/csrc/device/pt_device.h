@@ -1,0 +1,1181 @@
+/*
+ * pt_device.h -- CDNA4 (gfx950) device library of the MI355X path tracer.
+ *
+ * Embedded verbatim into every scene module that the runtime generates and
+ * compiles with hiprtc (runtime.cpp, codegen.cpp).  A scene module is this
+ * header + one generated `struct Scene` whose geometry is a compile-time CSG
+ * type (Sph/Pln/Uni/Isect/Diff/Xf nodes with their parameters at fixed offsets
+ * of the scene parameter block P) and whose materials are compile-time texture
+ * trees.  All per-scene control flow is therefore static and every node's
+ * state lives in VGPRs; scene constants are scalar loads from P.
+ *
+ * Execution model (one 64-lane wavefront = one workgroup):
+ *   - a wave owns a chunk of 64 consecutive (pixel, sample) items and traces
+ *     them one after another; the ray tree of one sample is walked by all 64
+ *     lanes together with wave-uniform state (the "spine": camera ray, mirror
+ *     and refraction chains, non-leaf children) and an explicit frame stack in
+ *     LDS instead of the reference's recursion (include/path-trace.h:58-165);
+ *   - a scatter loop with scatter_coefficient > eps (path-trace.h:138-163) is a
+ *     BURST: the wave evaluates 64 rejection attempts at once, lane l jumping
+ *     the PCG stream 3*l draws ahead (O(1) LCG jump), ballots accept / fail /
+ *     non-leaf masks, replays the reference's sequential consumption rule with
+ *     scalar bit arithmetic, queues accepted leaf children in LDS and traces
+ *     them 64 at a time, one child per lane;
+ *   - a leaf child (depth-1 <= 0 or child strength < eps: path-trace.h:105-108)
+ *     draws no random numbers, so children of a burst are independent and
+ *     the RNG stream and every branch stay bit-identical to the reference.
+ *
+ * Arithmetic: compiled with -ffp-contract=off and correctly rounded f32
+ * division/sqrt; every expression keeps the reference's evaluation order, so
+ * per-sample radiance is bit-identical to the reference in PT_ORDER_REFERENCE
+ * and to the oracle's group-64 order in the fast path (children of a burst
+ * batch are summed by a 64-wide pairwise butterfly, padded with -0.0f).
+ */
+#ifndef PT_DEVICE_H
+#define PT_DEVICE_H
+
+typedef unsigned long long u64;
+typedef unsigned int u32;
+
+namespace ptd
+{
+
+constexpr float EPS = 1e-3f;      /* include/misc.h:7 */
+constexpr float MAXV = 1e20f;     /* include/misc.h:8 */
+constexpr u64 PCG_MULT = 6364136223846793005ull;
+
+/* -------------------------------------------------------------- launch --- */
+struct PtImage
+{
+    const float4 *data; /* RGBA, row 0 = top */
+    u32 w, h;
+};
+
+struct PtLaunch
+{
+    u64 seed;
+    long long n_items;  /* items in this launch: slot-major, nsamp samples per slot */
+    long long chunk0;   /* first chunk (64 items) of this launch                   */
+    int W, H;
+    float sw, sh, dist;
+    int depth;
+    int nsamp;          /* samples per pixel slot in this pass                     */
+    int s0;             /* first sample index of this pass                         */
+    int pad0, pad1;
+};
+
+struct Env
+{
+    const float *__restrict__ P;
+    const PtImage *__restrict__ img;
+};
+
+/* ---------------------------------------------------------------- math --- */
+struct V3
+{
+    float x, y, z;
+};
+__device__ __forceinline__ V3 mk(float x, float y, float z)
+{
+    V3 r;
+    r.x = x, r.y = y, r.z = z;
+    return r;
+}
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 operator*(float s, V3 a) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 operator/(V3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ V3 operator-(V3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ bool is_zero(V3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+/* Vector3D dot: products then (x + y) + z, vector3d.h:102-106 */
+__device__ __forceinline__ float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ float length(V3 v) { return __builtin_sqrtf(dot(v, v)); }
+__device__ __forceinline__ V3 normalize(V3 v)
+{
+    float m = length(v);
+    if (m == 0.0f)
+        m = 1.0f;
+    return v / m;
+}
+/* (int)x as x86 cvttss2si: out-of-range and NaN give INT_MIN (the reference
+ * runs on x86; v_cvt_i32_f32 would saturate / give 0). */
+__device__ __forceinline__ int cvt_x86(float x)
+{
+    return (x != x || x >= 2147483648.0f || x < -2147483648.0f) ? (int)0x80000000 : (int)x;
+}
+__device__ __forceinline__ float clamp01(float x)
+{
+    float m = (x < 1.0f) ? x : 1.0f;  /* std::min(1.0f, x) */
+    return (0.0f < m) ? m : 0.0f;     /* std::max(0.0f, m) */
+}
+/* Vector3D::reflect, vector3d.h:186-190 */
+__device__ __forceinline__ V3 reflect(V3 d, V3 n)
+{
+    n = normalize(n);
+    return d - (2.0f * dot(d, n)) * n;
+}
+__device__ __forceinline__ bool bad_ior(float ior, V3 n, V3 d)
+{
+    return ior < EPS || ior > 1.0f / EPS || is_zero(n) || is_zero(d);
+}
+/* Vector3D::refractStrength, vector3d.h:191-202 -- the final sqrt(sqrt(x)) is
+ * ::sqrt(double) in the reference build: two double roots, one rounding. */
+__device__ __forceinline__ float refract_strength(V3 d, float ior, V3 n)
+{
+    if (bad_ior(ior, n, d))
+        return 0.0f;
+    n = normalize(n);
+    V3 inc = normalize(d);
+    float c = dot(inc, n);
+    float r = 1.0f - ior * ior * (1.0f - c * c);
+    if (r <= 0.0f)
+        return 0.0f;
+    return (float)__builtin_sqrt(__builtin_sqrt((double)r));
+}
+/* Vector3D::refract, vector3d.h:203-214 */
+__device__ __forceinline__ V3 refract(V3 d, float ior, V3 n)
+{
+    if (bad_ior(ior, n, d))
+        return mk(0, 0, 0);
+    n = normalize(n);
+    V3 inc = normalize(d);
+    float c = dot(inc, n);
+    float arg = 1.0f - ior * ior * (1.0f - c * c);
+    if (arg < 0.0f)
+        return mk(0, 0, 0);
+    return normalize(ior * inc - (ior * c + __builtin_sqrtf(arg)) * n);
+}
+/* Matrix::apply / applyNoTranslate, transform.h:408-421; m in ctor order */
+__device__ __forceinline__ V3 m_apply(const float *__restrict__ m, V3 v)
+{
+    return mk(((v.x * m[0] + v.y * m[1]) + v.z * m[2]) + m[3], ((v.x * m[4] + v.y * m[5]) + v.z * m[6]) + m[7],
+              ((v.x * m[8] + v.y * m[9]) + v.z * m[10]) + m[11]);
+}
+__device__ __forceinline__ V3 m_lin(const float *__restrict__ m, V3 v)
+{
+    return mk((v.x * m[0] + v.y * m[1]) + v.z * m[2], (v.x * m[4] + v.y * m[5]) + v.z * m[6],
+              (v.x * m[8] + v.y * m[9]) + v.z * m[10]);
+}
+
+/* ----------------------------------------------------------------- rng --- */
+/* PCG32 per (pixel, sample) -- include/pt/pt_engine.h is the specification. */
+struct Rng
+{
+    u64 st, inc;
+};
+__device__ __forceinline__ u64 splitmix64(u64 x)
+{
+    u64 z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ u32 pcg_out(u64 old)
+{
+    u32 xs = (u32)(((old >> 18) ^ old) >> 27);
+    u32 rot = (u32)(old >> 59);
+    return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+__device__ __forceinline__ void rng_seed(Rng &r, u64 seed, u64 pixel, u64 sample)
+{
+    u64 key = splitmix64(seed) ^ (pixel << 20) ^ sample;
+    r.st = splitmix64(key);
+    r.inc = (splitmix64(key ^ 0xD1B54A32D192ED03ull) << 1) | 1ull;
+}
+__device__ __forceinline__ u32 rng_next(Rng &r)
+{
+    u64 old = r.st;
+    r.st = old * PCG_MULT + r.inc;
+    return pcg_out(old);
+}
+/* uniform_real_distribution<float>, vector3d.h:22-33, for (0,1) and (-1,1) */
+__device__ __forceinline__ float u01(u32 o) { return (float)o / 4294967296.0f; }
+__device__ __forceinline__ float u11(u32 o)
+{
+    float r = (float)o / 4294967296.0f;
+    r *= 2.0f;
+    r += -1.0f;
+    return r;
+}
+
+/* ----------------------------------------------------------- CSG spans --- */
+/* Compact span: a boundary is (t, ref); the reference's normal and material
+ * (include/span.h:12-120) are functions of ref and recomputed only for the
+ * chosen hit.  ref = prim << 14 | material << 2 | end << 1 | flip. */
+struct CS
+{
+    float t0, t1;
+    u32 r0, r1;
+};
+constexpr u32 FLIP = 1u;
+__device__ __forceinline__ constexpr u32 mkref(int prim, int mat, int end)
+{
+    return ((u32)prim << 14) | ((u32)mat << 2) | ((u32)end << 1);
+}
+__device__ __forceinline__ int ref_mat(u32 r) { return (int)((r >> 2) & 0xFFFu); }
+__device__ __forceinline__ int ref_prim(u32 r) { return (int)(r >> 14); }
+__device__ __forceinline__ int ref_end(u32 r) { return (int)((r >> 1) & 1u); }
+/* span.h:93-119; copyEndFromStart / copyStartFromEnd negate the normal */
+__device__ __forceinline__ void end_from_end(CS &a, const CS &b) { a.t1 = b.t1, a.r1 = b.r1; }
+__device__ __forceinline__ void end_from_start(CS &a, const CS &b) { a.t1 = b.t0, a.r1 = b.r0 ^ FLIP; }
+__device__ __forceinline__ void start_from_end(CS &a, const CS &b) { a.t0 = b.t1, a.r0 = b.r1 ^ FLIP; }
+__device__ __forceinline__ void start_from_start(CS &a, const CS &b) { a.t0 = b.t0, a.r0 = b.r0; }
+
+/* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r. */
+template <int PRIM, int OFF, int MAT>
+struct Sph
+{
+    static constexpr int LO = PRIM, HI = PRIM + 1;
+    struct Ctx
+    {
+        V3 omc;
+        float c;
+    };
+    struct St
+    {
+        float t0, t1;
+        bool live;
+    };
+    __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)
+    {
+        c.omc = o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
+        c.c = dot(c.omc, c.omc) - e.P[OFF + 3];
+    }
+    __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float a, const Env &)
+    {
+        float b = dot(c.omc, d);
+        float disc = b * b - a * c.c;
+        s.live = !(disc <= EPS);
+        if (s.live) {
+            float q = __builtin_sqrtf(disc);
+            s.t0 = (-b - q) / a;
+            s.t1 = (-b + q) / a;
+        }
+    }
+    __device__ static __forceinline__ bool pull(St &s, CS &out)
+    {
+        if (!s.live)
+            return false;
+        out.t0 = s.t0, out.t1 = s.t1;
+        out.r0 = mkref(PRIM, MAT, 0), out.r1 = mkref(PRIM, MAT, 1);
+        s.live = false;
+        return true;
+    }
+    __device__ static __forceinline__ V3 normal(int, float t, V3 o, V3 d, const Env &e)
+    {
+        return normalize((o + t * d) - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+    }
+};
+
+/* Plane half-space {p : n.p + d < 0} (src/plane.cpp:35-63).  P[OFF..] = n, d. */
+template <int PRIM, int OFF, int MAT>
+struct Pln
+{
+    static constexpr int LO = PRIM, HI = PRIM + 1;
+    struct Ctx
+    {
+        float num;
+    };
+    struct St
+    {
+        float t0, t1;
+        bool live;
+    };
+    __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)
+    {
+        c.num = -e.P[OFF + 3] - dot(o, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+    }
+    __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float, const Env &e)
+    {
+        float div = dot(d, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+        float t = 0.0f;
+        bool deg = __builtin_fabsf(div) < EPS * EPS;
+        if (!deg) {
+            t = c.num / div;
+            deg = __builtin_fabsf(t) >= MAXV;
+        }
+        if (deg) {
+            s.live = __builtin_fabsf(c.num) < EPS * EPS;
+            s.t0 = -MAXV, s.t1 = MAXV;
+        } else if (div < 0.0f) {
+            s.live = true;
+            s.t0 = t, s.t1 = MAXV;
+        } else {
+            s.live = true;
+            s.t0 = -MAXV, s.t1 = t;
+        }
+    }
+    __device__ static __forceinline__ bool pull(St &s, CS &out)
+    {
+        if (!s.live)
+            return false;
+        out.t0 = s.t0, out.t1 = s.t1;
+        out.r0 = mkref(PRIM, MAT, 0), out.r1 = mkref(PRIM, MAT, 1);
+        s.live = false;
+        return true;
+    }
+    __device__ static __forceinline__ V3 normal(int, float, V3, V3, const Env &e)
+    {
+        return normalize(mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+    }
+};
+
+/* Binary CSG nodes: pull-protocol restatement of the reference iterators.
+ * init() preloads the first span of each child (the reference's nextA(),
+ * nextB() in init); pull() is the body of next() producing one span. */
+#define PTD_BINARY_COMMON                                                                           \
+    static constexpr int LO = A::LO, HI = B::HI;                                                    \
+    struct Ctx                                                                                      \
+    {                                                                                               \
+        typename A::Ctx a;                                                                          \
+        typename B::Ctx b;                                                                          \
+    };                                                                                              \
+    struct St                                                                                       \
+    {                                                                                               \
+        typename A::St a;                                                                           \
+        typename B::St b;                                                                           \
+        CS sa, sb;                                                                                  \
+        bool ea, eb;                                                                                \
+    };                                                                                              \
+    __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)                        \
+    {                                                                                               \
+        A::prep(c.a, o, e);                                                                         \
+        B::prep(c.b, o, e);                                                                         \
+    }                                                                                               \
+    __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float a, const Env &e) \
+    {                                                                                               \
+        A::init(s.a, c.a, d, a, e);                                                                 \
+        B::init(s.b, c.b, d, a, e);                                                                 \
+        s.ea = !A::pull(s.a, s.sa);                                                                 \
+        s.eb = !B::pull(s.b, s.sb);                                                                 \
+    }                                                                                               \
+    __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)       \
+    {                                                                                               \
+        if (prim < A::HI)                                                                           \
+            return A::normal(prim, t, o, d, e);                                                     \
+        return B::normal(prim, t, o, d, e);                                                         \
+    }
+
+/* src/union.cpp:84-134 */
+template <class A, class B>
+struct Uni
+{
+    PTD_BINARY_COMMON
+    __device__ static __forceinline__ bool pull(St &s, CS &out)
+    {
+        for (;;) {
+            if (s.ea) {
+                if (s.eb)
+                    return false;
+                out = s.sb;
+                s.eb = !B::pull(s.b, s.sb);
+                return true;
+            }
+            if (s.eb) {
+                out = s.sa;
+                s.ea = !A::pull(s.a, s.sa);
+                return true;
+            }
+            if (s.sa.t1 < s.sb.t0) {
+                out = s.sa;
+                s.ea = !A::pull(s.a, s.sa);
+                return true;
+            }
+            if (s.sb.t1 < s.sa.t0) {
+                out = s.sb;
+                s.eb = !B::pull(s.b, s.sb);
+                return true;
+            }
+            if (s.sa.t0 < s.sb.t0) {
+                if (s.sa.t1 < s.sb.t1)
+                    end_from_end(s.sa, s.sb);
+                s.eb = !B::pull(s.b, s.sb);
+            } else {
+                if (s.sa.t1 > s.sb.t1)
+                    end_from_end(s.sb, s.sa);
+                s.ea = !A::pull(s.a, s.sa);
+            }
+        }
+    }
+};
+
+/* src/intersection.cpp:84-130 */
+template <class A, class B>
+struct Isect
+{
+    PTD_BINARY_COMMON
+    __device__ static __forceinline__ bool pull(St &s, CS &out)
+    {
+        for (;;) {
+            if (s.ea || s.eb)
+                return false;
+            if (s.sa.t1 < s.sb.t0) {
+                s.ea = !A::pull(s.a, s.sa);
+                continue;
+            }
+            if (s.sb.t1 < s.sa.t0) {
+                s.eb = !B::pull(s.b, s.sb);
+                continue;
+            }
+            if (s.sa.t0 < s.sb.t0) {
+                if (s.sa.t1 < s.sb.t1) {
+                    start_from_start(s.sa, s.sb);
+                    out = s.sa;
+                    s.ea = !A::pull(s.a, s.sa);
+                    return true;
+                }
+                out = s.sb;
+                s.eb = !B::pull(s.b, s.sb);
+                return true;
+            }
+            if (s.sb.t1 < s.sa.t1) {
+                start_from_start(s.sb, s.sa);
+                out = s.sb;
+                s.eb = !B::pull(s.b, s.sb);
+                return true;
+            }
+            out = s.sa;
+            s.ea = !A::pull(s.a, s.sa);
+            return true;
+        }
+    }
+};
+
+/* src/difference.cpp:84-135, including the :124-130 copyEndFromStart quirk */
+template <class A, class B>
+struct Diff
+{
+    PTD_BINARY_COMMON
+    __device__ static __forceinline__ bool pull(St &s, CS &out)
+    {
+        for (;;) {
+            if (s.ea)
+                return false;
+            if (s.eb) {
+                out = s.sa;
+                s.ea = !A::pull(s.a, s.sa);
+                return true;
+            }
+            if (s.sa.t1 < s.sb.t0) {
+                out = s.sa;
+                s.ea = !A::pull(s.a, s.sa);
+                return true;
+            }
+            if (s.sb.t1 < s.sa.t0) {
+                s.eb = !B::pull(s.b, s.sb);
+            } else if (s.sa.t0 < s.sb.t0) {
+                if (s.sa.t1 < s.sb.t1) {
+                    end_from_start(s.sa, s.sb);
+                    out = s.sa;
+                    s.ea = !A::pull(s.a, s.sa);
+                    return true;
+                }
+                out = s.sa;
+                end_from_start(out, s.sb);
+                start_from_end(s.sa, s.sb);
+                s.eb = !B::pull(s.b, s.sb);
+                return true;
+            } else {
+                if (s.sa.t1 > s.sb.t1) {
+                    end_from_start(s.sa, s.sb);
+                    s.eb = !B::pull(s.b, s.sb);
+                    continue;
+                }
+                s.ea = !A::pull(s.a, s.sa);
+            }
+        }
+    }
+};
+
+/* TransformedObject (include/object.h:26-76): the child sees the ray mapped by
+ * m; span normals are mapped back by normalize(inv.applyNoTranslate(n)).
+ * P[MOFF..+12] = m, P[IOFF..+12] = inverse(m) (transform.h:350-383, host). */
+template <int MOFF, int IOFF, class C>
+struct Xf
+{
+    static constexpr int LO = C::LO, HI = C::HI;
+    struct Ctx
+    {
+        typename C::Ctx c;
+    };
+    typedef typename C::St St;
+    __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e) { C::prep(c.c, m_apply(e.P + MOFF, o), e); }
+    __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float, const Env &e)
+    {
+        V3 dl = m_lin(e.P + MOFF, d);
+        C::init(s, c.c, dl, dot(dl, dl), e);
+    }
+    __device__ static __forceinline__ bool pull(St &s, CS &out) { return C::pull(s, out); }
+    __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)
+    {
+        V3 n = C::normal(prim, t, m_apply(e.P + MOFF, o), m_lin(e.P + MOFF, d), e);
+        return normalize(m_lin(e.P + IOFF, n));
+    }
+};
+
+/* First qualifying span of the root, traceRay's scan (path-trace.h:66-100). */
+template <class R>
+__device__ __forceinline__ bool first_hit(const typename R::Ctx &ctx, V3 d, const Env &e, float &t, u32 &ref,
+                                          bool &exit_hit)
+{
+    typename R::St st;
+    R::init(st, ctx, d, dot(d, d), e);
+    CS s;
+    while (R::pull(st, s)) {
+        if (s.t0 >= MAXV)
+            return false;
+        if (s.t0 >= EPS) {
+            t = s.t0, ref = s.r0, exit_hit = false;
+            return true;
+        }
+        if (s.t1 >= MAXV)
+            return false;
+        if (s.t1 >= EPS) {
+            t = s.t1, ref = s.r1, exit_hit = true;
+            return true;
+        }
+    }
+    return false;
+}
+
+/* ------------------------------------------------------------ textures --- */
+__device__ __forceinline__ float mean3(V3 c) { return ((c.x + c.y) + c.z) * (1.0f / 3.0f); } /* texture.h:14-18 */
+
+__device__ __forceinline__ V3 img_rgb(const PtImage &im, int x, int y)
+{
+    if (!im.data || y < 0 || (u32)y >= im.h || x < 0 || (u32)x >= im.w)
+        return mk(0, 0, 0);
+    float4 v = im.data[(u32)x + (u32)y * im.w];
+    return mk(v.x, v.y, v.z);
+}
+__device__ __forceinline__ float img_alpha(const PtImage &im, int x, int y)
+{
+    if (!im.data || y < 0 || (u32)y >= im.h || x < 0 || (u32)x >= im.w)
+        return 0.0f;
+    return im.data[(u32)x + (u32)y * im.w].w;
+}
+/* ImageTexture texel (image_texture.h:20-27): `x -= floor(x)` runs in double */
+__device__ __forceinline__ void planar_texel(const PtImage &im, V3 v, int &xi, int &yi)
+{
+    float x = v.x, y = v.y;
+    x = (float)((double)x - __builtin_floor((double)x));
+    y = (float)((double)y - __builtin_floor((double)y));
+    y = 1.0f - y;
+    x *= (float)im.w;
+    y *= (float)im.h;
+    xi = cvt_x86(__builtin_floorf(x));
+    yi = cvt_x86(__builtin_floorf(y));
+}
+__device__ __forceinline__ int skybox_face(V3 v, float &fx, float &fy) /* image_texture.h:94-109 */
+{
+    V3 a = mk(__builtin_fabsf(v.x), __builtin_fabsf(v.y), __builtin_fabsf(v.z));
+    if (a.x > a.y && a.x > a.z) {
+        if (v.x < 0.0f) {
+            fx = -v.z / a.x, fy = v.y / a.x;
+            return 2; /* left */
+        }
+        fx = v.z / a.x, fy = v.y / a.x;
+        return 3; /* right */
+    }
+    if (a.y > a.z) {
+        if (v.y < 0.0f) {
+            fx = -v.x / a.y, fy = v.z / a.y;
+            return 1; /* bottom */
+        }
+        fx = v.x / a.y, fy = v.z / a.y;
+        return 0; /* top */
+    }
+    if (v.z < 0.0f) {
+        fx = v.x / a.z, fy = v.y / a.z;
+        return 5; /* back */
+    }
+    fx = -v.x / a.z, fy = v.y / a.z;
+    return 4; /* front */
+}
+__device__ __forceinline__ void skybox_texel(const PtImage &im, float x, float y, int &xi, int &yi)
+{
+    x = (float)((double)x * 0.5 + 0.5);
+    y = (float)(0.5 - (double)y * 0.5);
+    x *= (float)im.w;
+    y *= (float)im.h;
+    xi = cvt_x86(__builtin_floorf(x));
+    yi = cvt_x86(__builtin_floorf(y));
+}
+
+template <int OFF>
+struct TConst /* ColorTexture */
+{
+    __device__ static __forceinline__ V3 color(V3, const Env &e) { return mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]); }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return mean3(color(p, e)); }
+};
+struct TCoord /* test instrument */
+{
+    __device__ static __forceinline__ V3 color(V3 p, const Env &) { return p; }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return mean3(color(p, e)); }
+};
+template <int MOFF, class T>
+struct TXf /* TransformedTexture */
+{
+    __device__ static __forceinline__ V3 color(V3 p, const Env &e) { return T::color(m_apply(e.P + MOFF, p), e); }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return T::value(m_apply(e.P + MOFF, p), e); }
+};
+template <int SLOT>
+struct TImage /* ImageTexture */
+{
+    __device__ static __forceinline__ V3 color(V3 p, const Env &e)
+    {
+        int x, y;
+        planar_texel(e.img[SLOT], p, x, y);
+        return img_rgb(e.img[SLOT], x, y);
+    }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return mean3(color(p, e)); }
+};
+template <int SLOT>
+struct TImageAlpha /* ImageAlphaTexture */
+{
+    __device__ static __forceinline__ float value(V3 p, const Env &e)
+    {
+        int x, y;
+        planar_texel(e.img[SLOT], p, x, y);
+        return img_alpha(e.img[SLOT], x, y);
+    }
+    __device__ static __forceinline__ V3 color(V3 p, const Env &e)
+    {
+        float a = value(p, e);
+        return mk(a, a, a);
+    }
+};
+template <int S0, int S1, int S2, int S3, int S4, int S5>
+struct TSkybox /* ImageSkyboxTexture: top bottom left right front back */
+{
+    __device__ static __forceinline__ V3 color(V3 v, const Env &e)
+    {
+        if (is_zero(v))
+            return mk(0, 0, 0);
+        float fx, fy;
+        int f = skybox_face(v, fx, fy);
+        const int slots[6] = {S0, S1, S2, S3, S4, S5};
+        const PtImage &im = e.img[slots[f]];
+        int x, y;
+        skybox_texel(im, fx, fy, x, y);
+        return img_rgb(im, x, y);
+    }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return mean3(color(p, e)); }
+};
+template <int S0, int S1, int S2, int S3, int S4, int S5>
+struct TSkyboxAlpha /* ImageSkyboxAlphaTexture */
+{
+    __device__ static __forceinline__ float value(V3 v, const Env &e)
+    {
+        if (is_zero(v))
+            return 0.0f;
+        float fx, fy;
+        int f = skybox_face(v, fx, fy);
+        const int slots[6] = {S0, S1, S2, S3, S4, S5};
+        const PtImage &im = e.img[slots[f]];
+        int x, y;
+        skybox_texel(im, fx, fy, x, y);
+        return img_alpha(im, x, y);
+    }
+    __device__ static __forceinline__ V3 color(V3 v, const Env &e)
+    {
+        float a = value(v, e);
+        return mk(a, a, a);
+    }
+};
+template <int OFF, class T>
+struct TMul /* MultiplyTexture */
+{
+    __device__ static __forceinline__ V3 color(V3 p, const Env &e)
+    {
+        return T::color(p, e) * mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
+    }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return mean3(color(p, e)); }
+};
+__device__ __forceinline__ float log_filter(float v) /* filter_texture.h:66-71 */
+{
+    if ((double)v <= 1e-30)
+        return 0.0f;
+    return 0.5f + (float)__builtin_log((double)v) / 0.693147182f / 256.0f;
+}
+template <class T>
+struct TLog /* LogTexture */
+{
+    __device__ static __forceinline__ V3 color(V3 p, const Env &e)
+    {
+        V3 c = T::color(p, e);
+        return mk(log_filter(c.x), log_filter(c.y), log_filter(c.z));
+    }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return mean3(color(p, e)); }
+};
+__device__ __forceinline__ V3 mirrorball_map(V3 v) /* transform_texture.h:46-59 */
+{
+    if (is_zero(v))
+        return mk(0, 0, 0);
+    v = normalize(v);
+    if (v.z <= -1.0f)
+        return mk(0, 0.5f, 0);
+    float d = __builtin_sqrtf(2.0f + 2.0f * v.z);
+    if (d == 0.0f)
+        return mk(0, 0.5f, 0);
+    float xt = v.x / d, yt = v.y / d;
+    return mk((float)((double)xt * 0.5 + 0.5), (float)((double)yt * 0.5 + 0.5), 0);
+}
+__device__ __forceinline__ V3 spherical_map(V3 v) /* transform_texture.h:73-85 */
+{
+    const double PI = 3.14159265358979323846;
+    if (is_zero(v))
+        return mk(0, 0, 0);
+    v = normalize(v);
+    float theta = (float)__builtin_atan2((double)v.y, (double)v.x);
+    if ((double)theta < -PI)
+        theta = (float)((double)theta + 2 * PI);
+    if ((double)theta > PI)
+        theta = (float)((double)theta - 2 * PI);
+    float phi = (float)__builtin_asin((double)v.z);
+    return mk((float)((double)theta * 0.5 / PI + 0.5), (float)((double)phi / (PI / 2) * 0.5 + 0.5), 0);
+}
+template <class T>
+struct TMirrorBall
+{
+    __device__ static __forceinline__ V3 color(V3 p, const Env &e) { return T::color(mirrorball_map(p), e); }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return T::value(mirrorball_map(p), e); }
+};
+template <class T>
+struct TSpherical
+{
+    __device__ static __forceinline__ V3 color(V3 p, const Env &e) { return T::color(spherical_map(p), e); }
+    __device__ static __forceinline__ float value(V3 p, const Env &e) { return T::value(spherical_map(p), e); }
+};
+
+/* --------------------------------------------------------- wave helpers --- */
+__device__ __forceinline__ float rdlane(float v, int l)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+__device__ __forceinline__ V3 univ(V3 v) { return mk(unif(v.x), unif(v.y), unif(v.z)); }
+__device__ __forceinline__ int nth_set_bit(u64 m, int k) /* 1-based k, m has >= k bits */
+{
+    for (int j = 1; j < k; j++)
+        m &= m - 1;
+    return __builtin_ctzll(m);
+}
+/* 64-wide pairwise butterfly: lane i adds lane i^k for k = 1..32; IEEE
+ * addition is commutative so every lane ends with the same tree sum. */
+__device__ __forceinline__ float wave_tree_sum(float v)
+{
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1)
+        v = v + __shfl_xor(v, k, 64);
+    return v;
+}
+
+struct Counters
+{
+    u64 queries, leaf, attempts, rounds, shaded, nonleaf;
+};
+
+/* ---------------------------------------------------------------- spine --- */
+struct Frame /* one suspended traceRay activation (LDS) */
+{
+    V3 d;
+    float strength;
+    V3 hit;
+    int depth;
+    V3 n;
+    int mat;
+    V3 retval;
+    float add;
+    V3 refl;
+    float rf;
+    V3 rc;
+    float sc;
+    V3 w;
+    int N;
+    int i;
+    int resume;
+    int pad0, pad1;
+};
+
+enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
+
+/* Wave-cooperative scatter loop (path-trace.h:138-163) for sc > eps, from
+ * child index i.  Returns B_DONE when all N children are summed, B_ABORT on the
+ * reference's count > 1000 early return (path-trace.h:149-152), B_NONLEAF with
+ * the next child's direction/factor when that child must recurse (it draws
+ * random numbers, so it runs on the spine). */
+template <class S, bool STRICT>
+__device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
+                                     float4 *q, V3 hit, V3 n, V3 refl, V3 rc, float sc, float strength, float add,
+                                     int depth, int N, int &i, V3 &retval, V3 &nl_dir, float &nl_factor,
+                                     Counters &cnt)
+{
+    const int lane = threadIdx.x;
+    const V3 kR = (1.0f / sc - 1.0f) * refl;          /* (1 / scatter_coefficient - 1) * reflectedRayDir */
+    const float sNa = (strength / (float)N) * add;    /* strength / scatter_ray_count * addFactor          */
+    const float aN = add / (float)N;                  /* addFactor / scatter_ray_count                      */
+    const float abs_rc = length(rc);
+    const bool child_leaf_depth = depth - 1 <= 0;
+    typename S::Root::Ctx ctx;
+    S::Root::prep(ctx, hit, e);
+    const u64 ginc = G3l * rng.inc;
+    int qhead = 0, qn = 0, fails = 0, reason = -1;
+    for (;;) {
+        if (reason < 0 && qn < 64) {
+            /* ---- generation round: lane l evaluates attempt l (draws 3l..3l+2) */
+            const int rem = N - (i + qn);
+            u64 s0 = A3l * rng.st + ginc;
+            u64 s1 = s0 * PCG_MULT + rng.inc;
+            u64 s2 = s1 * PCG_MULT + rng.inc;
+            V3 v = mk(u11(pcg_out(s0)), u11(pcg_out(s1)), u11(pcg_out(s2)));
+            bool ball = !(length(v) > 1.0f);                 /* rand(): while (mag > max) */
+            V3 w = v + kR;
+            bool hemi = !(dot(n, w) <= EPS);                 /* while (dot(normal, dir) <= eps) */
+            bool acc = ball && hemi;
+            V3 wn = mk(0, 0, 0);
+            float factor = 0.0f;
+            bool leaf = true;
+            if (acc) {
+                wn = normalize(w);
+                factor = 1.0f - (1.0f - dot(wn, n)) * sc;
+                float cs = (sNa * factor) * abs_rc;
+                leaf = child_leaf_depth || cs < EPS;
+            }
+            const u64 A = __ballot(acc), F = __ballot(ball && !hemi), NL = __ballot(acc && !leaf);
+            cnt.rounds++;
+            /* ---- replay the sequential consumption rule on the masks */
+            const int nl = NL ? __builtin_ctzll(NL) : 64;
+            const int pos_rem = (__popcll(A) >= (unsigned)rem) ? nth_set_bit(A, rem) : 64;
+            int pos_abort = 64;
+            if (fails + __popcll(F) >= 1000) {
+                int f = fails;
+                for (int l = 0; l < 64; l++) {
+                    if (l == nl || l == pos_rem)
+                        break;
+                    if ((A >> l) & 1ull)
+                        f = 0;
+                    else if ((F >> l) & 1ull) {
+                        if (++f == 1000) {
+                            pos_abort = l;
+                            break;
+                        }
+                    }
+                }
+            }
+            int cut = 63;
+            u64 take; /* accepted leaf attempts consumed this round */
+            if (pos_abort < 64 && pos_abort < nl && pos_abort < pos_rem) {
+                reason = B_ABORT, cut = pos_abort;
+                take = A & ((1ull << cut) - 1ull);
+            } else if (nl < 64 && nl <= pos_rem) {
+                reason = B_NONLEAF, cut = nl;
+                take = A & ((1ull << cut) - 1ull);
+                nl_dir = mk(rdlane(wn.x, nl), rdlane(wn.y, nl), rdlane(wn.z, nl));
+                nl_factor = rdlane(factor, nl);
+            } else if (pos_rem < 64) {
+                reason = B_DONE, cut = pos_rem;
+                take = (cut == 63) ? A : (A & ((2ull << cut) - 1ull));
+            } else {
+                take = A;
+                if (A) {
+                    int last = 63 - __builtin_clzll(A);
+                    fails = (last == 63) ? 0 : __popcll(F >> (last + 1));
+                } else {
+                    fails += __popcll(F);
+                }
+            }
+            cnt.attempts += (u64)(cut + 1);
+            if ((take >> lane) & 1ull) {
+                int r = __popcll(take & ((1ull << lane) - 1ull));
+                q[(qhead + qn + r) & 127] = make_float4(wn.x, wn.y, wn.z, factor);
+            }
+            qn += __popcll(take);
+            /* ---- advance the sample's stream past the consumed attempts */
+            const int m = cut + 1;
+            rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
+        }
+        if (qn >= 64 || (reason >= 0 && qn > 0)) {
+            /* ---- trace one batch of leaf children, one per lane */
+            const int cntb = qn < 64 ? qn : 64;
+            V3 term = mk(-0.0f, -0.0f, -0.0f);
+            if (lane < cntb) {
+                float4 en = q[(qhead + lane) & 127];
+                V3 dir = mk(en.x, en.y, en.z);
+                float t;
+                u32 ref;
+                bool ex;
+                V3 col = mk(0, 0, 0);
+                if (first_hit<typename S::Root>(ctx, dir, e, t, ref, ex))
+                    col = S::emis(ref_mat(ref), hit + t * dir, e);
+                term = ((aN * en.w) * rc) * col;
+            }
+            if (STRICT) {
+                for (int j = 0; j < cntb; j++)
+                    retval = retval + mk(rdlane(term.x, j), rdlane(term.y, j), rdlane(term.z, j));
+            } else {
+                retval = retval + mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
+                retval = univ(retval);
+            }
+            cnt.leaf += (u64)cntb;
+            qhead += cntb;
+            qn -= cntb;
+            i += cntb;
+            continue;
+        }
+        if (reason >= 0)
+            return reason;
+    }
+}
+
+enum { PH_ENTER, PH_SETUP, PH_LOOP, PH_RETURN };
+enum { RS_REFRACT, RS_SCATTER };
+
+/* One sample = one traceRay tree (path-trace.h:58-165) + the jittered camera
+ * ray of tracePixel (path-trace.h:190-198). */
+template <class S, int MAXD, bool STRICT>
+__device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *stk, float4 *q,
+                                           const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt)
+{
+    const int lane = threadIdx.x;
+    Rng rng;
+    rng_seed(rng, lp.seed, (u64)pix, (u64)s);
+    const int px = pix % lp.W, py = pix / lp.W;
+    float x = 2.0f * ((float)px + u01(rng_next(rng))) / (float)lp.W - 1.0f;
+    float y = 1.0f - 2.0f * ((float)py + u01(rng_next(rng))) / (float)lp.H;
+    V3 o = mk(0, 0, 0), d = mk(x * lp.sw, y * lp.sh, -lp.dist);
+    float strength = 1.0f;
+    int depth = lp.depth;
+    int sp = 0;
+    V3 result = mk(0, 0, 0);
+    V3 hit = mk(0, 0, 0), n = mk(0, 0, 0), retval = mk(0, 0, 0), refl = mk(0, 0, 0), rc = mk(0, 0, 0),
+       w = mk(0, 0, 0);
+    int mat = 0, N = 1, i = 0, resume = 0;
+    float add = 1.0f, rf = 0.0f, sc = 0.0f;
+    int phase = PH_ENTER;
+
+#define PTD_PUSH_AND_ENTER(RES, DIR, STRENGTH)                                                          \
+    do {                                                                                                \
+        if (lane == 0) {                                                                                \
+            Frame &f = stk[sp];                                                                         \
+            f.d = d, f.strength = strength, f.hit = hit, f.depth = depth, f.n = n, f.mat = mat;         \
+            f.retval = retval, f.add = add, f.refl = refl, f.rf = rf, f.rc = rc, f.sc = sc, f.w = w;    \
+            f.N = N, f.i = i, f.resume = (RES);                                                         \
+        }                                                                                               \
+        sp++;                                                                                           \
+        o = hit, d = (DIR), strength = (STRENGTH), depth = depth - 1;                                   \
+        phase = PH_ENTER;                                                                               \
+    } while (0)
+
+    for (;;) {
+        if (phase == PH_ENTER) {
+            cnt.queries++;
+            typename S::Root::Ctx ctx;
+            S::Root::prep(ctx, o, e);
+            float t = 0.0f;
+            u32 ref = 0;
+            bool ex = false;
+            if (!first_hit<typename S::Root>(ctx, d, e, t, ref, ex)) {
+                result = mk(0, 0, 0);
+                phase = PH_RETURN;
+                continue;
+            }
+            hit = o + t * d;
+            mat = ref_mat(ref);
+            V3 nn = S::Root::normal(ref_prim(ref), t, o, d, e);
+            if (ref & FLIP)
+                nn = -nn;
+            float ior;
+            if (ex) {
+                n = -nn;
+                ior = S::ior(mat, e);
+            } else {
+                n = nn;
+                ior = (float)(1.0 / (double)S::ior(mat, e));
+            }
+            retval = S::emis(mat, hit, e);
+            add = 1.0f;
+            if (depth <= 0 || strength < EPS) {
+                result = retval;
+                phase = PH_RETURN;
+                continue;
+            }
+            cnt.shaded++;
+            rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
+            if (rf > EPS) {
+                V3 rd = refract(d, ior, n);
+                if (!is_zero(rd)) {
+                    V3 tr = S::trans(mat, hit, e);
+                    w = (add * rf) * tr;
+                    float cs = strength * rf * add * length(tr);
+                    PTD_PUSH_AND_ENTER(RS_REFRACT, rd, cs);
+                    continue;
+                }
+            }
+            phase = PH_SETUP;
+        } else if (phase == PH_SETUP) {
+            if (add < EPS) {
+                result = retval;
+                phase = PH_RETURN;
+                continue;
+            }
+            sc = clamp01(S::scat(mat, hit, e));
+            N = cvt_x86(10000.0f * strength * add * sc);
+            if (sc <= EPS)
+                N = 1;
+            if (N == 0)
+                N = 1;
+            rc = S::refl(mat, hit, e);
+            refl = reflect(d, n);
+            i = 0;
+            phase = PH_LOOP;
+        } else if (phase == PH_LOOP) {
+            if (i >= N) {
+                result = retval;
+                phase = PH_RETURN;
+                continue;
+            }
+            if (sc > EPS) {
+                V3 nd;
+                float nf;
+                int why = burst<S, STRICT>(e, rng, jump, A3l, G3l, q, hit, n, refl, rc, sc, strength, add, depth, N,
+                                           i, retval, nd, nf, cnt);
+                if (why != B_NONLEAF) {
+                    result = retval;
+                    phase = PH_RETURN;
+                    continue;
+                }
+                cnt.nonleaf++;
+                w = ((add / (float)N) * nf) * rc;
+                float cs = (((strength / (float)N) * add) * nf) * length(rc);
+                PTD_PUSH_AND_ENTER(RS_SCATTER, nd, cs);
+            } else {
+                float factor = 1.0f - (1.0f - dot(refl, n)) * sc;
+                w = ((add / (float)N) * factor) * rc;
+                float cs = (((strength / (float)N) * add) * factor) * length(rc);
+                PTD_PUSH_AND_ENTER(RS_SCATTER, refl, cs);
+            }
+        } else { /* PH_RETURN */
+            if (sp == 0)
+                break;
+            sp--;
+            const Frame &f = stk[sp];
+            d = f.d, strength = f.strength, hit = f.hit, depth = f.depth, n = f.n, mat = f.mat;
+            V3 r0 = f.retval;
+            add = f.add, refl = f.refl, rf = f.rf, rc = f.rc, sc = f.sc, w = f.w, N = f.N, i = f.i;
+            resume = f.resume;
+            retval = r0 + w * result;
+            if (resume == RS_REFRACT) {
+                add *= 1.0f - rf;
+                phase = PH_SETUP;
+            } else {
+                i += 1;
+                phase = PH_LOOP;
+            }
+        }
+    }
+#undef PTD_PUSH_AND_ENTER
+    /* tracePixel with one sample: (Color(0,0,0) + traceRay(...)) / 1 */
+    V3 z = mk(0, 0, 0);
+    return (z + result) / 1.0f;
+}
+
+/* The megakernel body: this wave traces items [64*chunk, 64*chunk + 64). */
+template <class S, int MAXD, bool STRICT>
+__device__ __forceinline__ void render_chunk(const float *__restrict__ P, const PtImage *__restrict__ imgs,
+                                             const u64 *__restrict__ jump, float *__restrict__ out,
+                                             const int *__restrict__ pixels, u64 *__restrict__ stats,
+                                             const PtLaunch &lp)
+{
+    __shared__ Frame stk[MAXD + 1];
+    __shared__ float4 q[128];
+    const int lane = threadIdx.x;
+    const Env e = {P, imgs};
+    const long long item0 = (lp.chunk0 + (long long)blockIdx.x) * 64;
+    const u64 A3l = jump[2 * lane], G3l = jump[2 * lane + 1];
+    Counters cnt = {0, 0, 0, 0, 0, 0};
+    V3 mine = mk(0, 0, 0);
+    for (int j = 0; j < 64; j++) {
+        const long long item = item0 + j;
+        if (item >= lp.n_items)
+            break;
+        const long long slot = item / lp.nsamp;
+        const int s = lp.s0 + (int)(item - slot * lp.nsamp);
+        const int pix = pixels ? pixels[slot] : (int)slot;
+        V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk, q, jump, A3l, G3l, cnt);
+        if (lane == j)
+            mine = c;
+    }
+    const long long my = item0 + lane;
+    if (my < lp.n_items) {
+        out[3 * my + 0] = mine.x;
+        out[3 * my + 1] = mine.y;
+        out[3 * my + 2] = mine.z;
+    }
+    if (lane == 0 && stats) {
+        atomicAdd(&stats[0], cnt.queries);
+        atomicAdd(&stats[1], cnt.leaf);
+        atomicAdd(&stats[2], cnt.attempts);
+        atomicAdd(&stats[3], cnt.rounds);
+        atomicAdd(&stats[4], cnt.shaded);
+        atomicAdd(&stats[5], cnt.nonleaf);
+    }
+}
+
+} // namespace ptd
+
+#define PT_RENDER_ARGS                                                                                     \
+    const float *__restrict__ P, const ptd::PtImage *__restrict__ imgs, const u64 *__restrict__ jump,      \
+        float *__restrict__ out, const int *__restrict__ pixels, u64 *__restrict__ stats, ptd::PtLaunch lp
+
+#define PT_DEFINE_KERNELS(SCENE, MAXD)                                                                      \
+    extern "C" __global__ __launch_bounds__(64) void pt_render_fast(PT_RENDER_ARGS)                         \
+    {                                                                                                       \
+        ptd::render_chunk<SCENE, MAXD, false>(P, imgs, jump, out, pixels, stats, lp);                      \
+    }                                                                                                       \
+    extern "C" __global__ __launch_bounds__(64) void pt_render_strict(PT_RENDER_ARGS)                       \
+    {                                                                                                       \
+        ptd::render_chunk<SCENE, MAXD, true>(P, imgs, jump, out, pixels, stats, lp);                       \
+    }
+
+#endif
+
+#ifndef PT_DEVICE_REDUCE_DEFINED
+#define PT_DEVICE_REDUCE_DEFINED
+/* Ordered per-pixel sample sum: acc = ((acc + x_0) + x_1) + ..., the
+ * accumulation order of tracePixel's spp loop (path-trace.h:192-199); on the
+ * last pass writes acc / spp to the frame buffer.  One thread per pixel slot. */
+extern "C" __global__ __launch_bounds__(256) void pt_reduce(const float *__restrict__ in, float *__restrict__ accum,
+                                                            float *__restrict__ fb, const int *__restrict__ pixels,
+                                                            long long nslots, int nsamp, int first, int last,
+                                                            float spp)
+{
+    const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= nslots)
+        return;
+    float ax = 0.0f, ay = 0.0f, az = 0.0f;
+    if (!first) {
+        ax = accum[3 * slot + 0];
+        ay = accum[3 * slot + 1];
+        az = accum[3 * slot + 2];
+    }
+    const float *p = in + 3 * slot * (long long)nsamp;
+    for (int s = 0; s < nsamp; s++) {
+        ax = ax + p[3 * s + 0];
+        ay = ay + p[3 * s + 1];
+        az = az + p[3 * s + 2];
+    }
+    if (last) {
+        const long long pix = pixels ? (long long)pixels[slot] : slot;
+        fb[3 * pix + 0] = ax / spp;
+        fb[3 * pix + 1] = ay / spp;
+        fb[3 * pix + 2] = az / spp;
+    } else {
+        accum[3 * slot + 0] = ax;
+        accum[3 * slot + 1] = ay;
+        accum[3 * slot + 2] = az;
+    }
+}
+#endif

@@ -1,0 +1,109 @@
+/* internal.h -- host-side data model of libpt.so (not part of the C ABI). */
+#ifndef PT_INTERNAL_H
+#define PT_INTERNAL_H
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/pt/pt.h"
+
+namespace pt
+{
+
+/* An error carrying a C-ABI status code; caught at every extern "C" boundary. */
+struct Error : std::runtime_error
+{
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+void set_error(const std::string &msg);
+
+/* Host copies of the reference scene graph, one record per constructor call. */
+struct ImageRec
+{
+    int w = 0, h = 0;
+    std::vector<float> rgba; /* row 0 = top */
+};
+
+enum class TexKind { Color, Image, ImageAlpha, Skybox, SkyboxAlpha, Multiply, Log, MirrorBall, Spherical, Xform, Coord };
+
+struct TexRec
+{
+    TexKind kind;
+    float f[12] = {0};
+    int child = -1;   /* inner texture */
+    int img[6] = {-1, -1, -1, -1, -1, -1};
+};
+
+struct MatRec
+{
+    int reflect, scatter, emissive, transmit, trc;
+    float ior;
+};
+
+enum class ObjKind { Sphere, Plane, Union, Intersection, Difference, Xform };
+
+struct ObjRec
+{
+    ObjKind kind;
+    float f[12] = {0}; /* sphere: c, r; plane: n, d; xform: m */
+    int mat = -1;
+    int a = -1, b = -1; /* children */
+};
+
+struct DeviceState; /* runtime.cpp */
+
+struct SceneImpl
+{
+    std::vector<ImageRec> images;
+    std::vector<TexRec> textures;
+    std::vector<MatRec> materials;
+    std::vector<ObjRec> objects;
+    int root = -1;
+    int default_tex[2] = {-1, -1}; /* lazily created ColorTexture(0), ColorTexture(1) */
+    std::map<int, std::unique_ptr<DeviceState>> devices;
+    std::string last_key;
+    void clear()
+    {
+        images.clear(), textures.clear(), materials.clear(), objects.clear();
+        root = -1;
+        default_tex[0] = default_tex[1] = -1;
+    }
+};
+
+/* Generated device module for one (scene, depth). */
+struct Generated
+{
+    std::string source;         /* full hiprtc translation unit                      */
+    std::string key;            /* content hash of source + options + compiler        */
+    std::vector<float> params;  /* scene parameter block P                           */
+    std::vector<int> image_ids; /* slot -> scene image index                          */
+    int maxd = 0;
+    int n_prims = 0, n_spheres = 0, n_planes = 0, n_mats = 0;
+};
+
+Generated generate(const SceneImpl &s, int depth);
+/* Returns the gfx950 code object for g (from the cache or compiled now). */
+const std::vector<char> &code_object(const Generated &g);
+
+/* Matrix helpers (reference include/transform.h arithmetic). */
+void mat_inverse(const float *m, float *out); /* throws Error(PT_ERR_MATH) */
+void mat_concat(const float *a, const float *b, float *out);
+void mat_rotate(const float *axis, double angle, float *out);
+
+/* Image I/O (reference src/image.cpp). */
+ImageRec read_hdr(const std::string &path);
+void write_hdr(const std::string &path, const float *rgb, int w, int h);
+void write_bmp(const std::string &path, const float *rgb, int w, int h, int count);
+
+std::string device_library_source(); /* embedded pt_device.h */
+
+} // namespace pt
+
+#endif

@@ -1,0 +1,941 @@
+/*
+ * runtime.cpp -- libpt.so: the C-ABI boundary (include/pt/pt.h).
+ *
+ * Holds the host copy of the scene graph built through the reference-shaped
+ * constructors, flattens it into a device module (codegen.cpp), gets the
+ * gfx950 code object (jit.cpp), and drives the megakernel:
+ *
+ *   items = (pixel slot, sample) pairs, slot-major; one wavefront per 64
+ *   consecutive items (pt_render_fast / pt_render_strict); each item's
+ *   radiance lands in a staging buffer; pt_reduce then sums every pixel's
+ *   samples in sample order and divides by spp, exactly tracePixel's loop.
+ *   Large frames run in sample passes bounded by max_buffer_bytes, the
+ *   running per-pixel sums carried between passes.
+ *
+ * This replaces RenderBlock::calcPixelColor's per-pixel tracePixel calls
+ * (reference src/test.cpp:441-465); the block farm / thread pool around it
+ * (src/test.cpp:147-518) becomes the hardware dispatcher plus, across GPUs,
+ * one process per device (bench.py / pathtrace.dist).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+
+#include "../../include/pt/pt_engine.h"
+#include "internal.h"
+
+struct pt_scene
+{
+    pt::SceneImpl impl;
+};
+
+namespace pt
+{
+
+thread_local std::string g_error;
+void set_error(const std::string &msg) { g_error = msg; }
+
+#define HIPCHECK(x)                                                                                  \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess)                                                                        \
+            throw Error(PT_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));              \
+    } while (0)
+
+struct PtImageDev
+{
+    const void *data;
+    uint32_t w, h;
+};
+
+struct PtLaunchHost /* must match ptd::PtLaunch */
+{
+    uint64_t seed;
+    long long n_items;
+    long long chunk0;
+    int W, H;
+    float sw, sh, dist;
+    int depth;
+    int nsamp;
+    int s0;
+    int pad0, pad1;
+};
+
+template <class T>
+struct DevBuf
+{
+    T *p = nullptr;
+    size_t n = 0;
+    void ensure(size_t count)
+    {
+        if (count <= n)
+            return;
+        release();
+        HIPCHECK(hipMalloc((void **)&p, count * sizeof(T)));
+        n = count;
+    }
+    void release()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct DeviceState
+{
+    int device = 0;
+    std::string key;
+    hipModule_t mod = nullptr;
+    hipFunction_t fast = nullptr, strict = nullptr, reduce = nullptr;
+    std::vector<float> params;
+    DevBuf<float> P;
+    DevBuf<PtImageDev> imgs;
+    std::vector<DevBuf<float>> img_data;
+    std::vector<int> img_ids;
+    DevBuf<uint64_t> jump;
+    DevBuf<float> stage, accum, fb;
+    DevBuf<int> pixels;
+    DevBuf<uint64_t> stats;
+    ~DeviceState()
+    {
+        int prev = 0;
+        if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(device) == hipSuccess) {
+            P.release(), imgs.release(), jump.release(), stage.release(), accum.release(), fb.release();
+            pixels.release(), stats.release();
+            for (auto &b : img_data) b.release();
+            if (mod)
+                (void)hipModuleUnload(mod);
+            (void)hipSetDevice(prev);
+        }
+    }
+};
+
+/* ------------------------------------------------------------ matrices -- */
+/* transform.h:342-383 */
+void mat_inverse(const float *m, float *out)
+{
+    const float x00 = m[0], x10 = m[1], x20 = m[2], x30 = m[3], x01 = m[4], x11 = m[5], x21 = m[6], x31 = m[7],
+                x02 = m[8], x12 = m[9], x22 = m[10], x32 = m[11];
+    float det = x00 * (x11 * x22 - x12 * x21) + x10 * (x02 * x21 - x01 * x22) + x20 * (x01 * x12 - x02 * x11);
+    if (det == 0.0f)
+        throw Error(PT_ERR_MATH, "can't invert singular matrix");
+    float f = 1.0f / det;
+    out[0] = (x11 * x22 - x12 * x21) * f;
+    out[1] = (x12 * x20 - x10 * x22) * f;
+    out[2] = (x10 * x21 - x11 * x20) * f;
+    out[3] = (-x10 * x21 * x32 + x11 * x20 * x32 + x10 * x22 * x31 - x12 * x20 * x31 - x11 * x22 * x30 +
+              x12 * x21 * x30) *
+             f;
+    out[4] = (x02 * x21 - x01 * x22) * f;
+    out[5] = (x00 * x22 - x02 * x20) * f;
+    out[6] = (x01 * x20 - x00 * x21) * f;
+    out[7] = (x00 * x21 * x32 - x01 * x20 * x32 - x00 * x22 * x31 + x02 * x20 * x31 + x01 * x22 * x30 -
+              x02 * x21 * x30) *
+             f;
+    out[8] = (x01 * x12 - x02 * x11) * f;
+    out[9] = (x02 * x10 - x00 * x12) * f;
+    out[10] = (x00 * x11 - x01 * x10) * f;
+    out[11] = (-x00 * x11 * x32 + x01 * x10 * x32 + x00 * x12 * x31 - x02 * x10 * x31 - x01 * x12 * x30 +
+               x02 * x11 * x30) *
+              f;
+}
+
+/* Matrix::concat, transform.h:391-406: this->concat(rt) = "apply this, then rt" */
+void mat_concat(const float *a, const float *b, float *out)
+{
+    const float t00 = a[0], t10 = a[1], t20 = a[2], t30 = a[3], t01 = a[4], t11 = a[5], t21 = a[6], t31 = a[7],
+                t02 = a[8], t12 = a[9], t22 = a[10], t32 = a[11];
+    const float r00 = b[0], r10 = b[1], r20 = b[2], r30 = b[3], r01 = b[4], r11 = b[5], r21 = b[6], r31 = b[7],
+                r02 = b[8], r12 = b[9], r22 = b[10], r32 = b[11];
+    out[0] = t00 * r00 + t01 * r10 + t02 * r20;
+    out[1] = t10 * r00 + t11 * r10 + t12 * r20;
+    out[2] = t20 * r00 + t21 * r10 + t22 * r20;
+    out[3] = t30 * r00 + t31 * r10 + t32 * r20 + r30;
+    out[4] = t00 * r01 + t01 * r11 + t02 * r21;
+    out[5] = t10 * r01 + t11 * r11 + t12 * r21;
+    out[6] = t20 * r01 + t21 * r11 + t22 * r21;
+    out[7] = t30 * r01 + t31 * r11 + t32 * r21 + r31;
+    out[8] = t00 * r02 + t01 * r12 + t02 * r22;
+    out[9] = t10 * r02 + t11 * r12 + t12 * r22;
+    out[10] = t20 * r02 + t21 * r12 + t22 * r22;
+    out[11] = t30 * r02 + t31 * r12 + t32 * r22 + r32;
+}
+
+/* Matrix::rotate, transform.h:207-225 (cos/sin of a double angle, float math) */
+void mat_rotate(const float *axis, double angle, float *out)
+{
+    float ax = axis[0], ay = axis[1], az = axis[2];
+    float m = std::sqrt((ax * ax + ay * ay) + az * az);
+    if (m == 0)
+        m = 1;
+    ax /= m, ay /= m, az /= m;
+    float c = (float)std::cos(angle), s = (float)std::sin(angle), v = 1 - c;
+    float xx = ax * ax, xy = ax * ay, xz = ax * az, yy = ay * ay, yz = ay * az, zz = az * az;
+    float r[12] = {xx + (1 - xx) * c, xy * v - az * s, xz * v + ay * s, 0, xy * v + az * s, yy + (1 - yy) * c,
+                   yz * v - ax * s,   0,               xz * v - ay * s, yz * v + ax * s, zz + (1 - zz) * c, 0};
+    memcpy(out, r, sizeof r);
+}
+
+/* -------------------------------------------------------------- helpers -- */
+namespace
+{
+
+SceneImpl &S(pt_scene *s)
+{
+    if (!s)
+        throw Error(PT_ERR_ARG, "null scene");
+    return s->impl;
+}
+
+void check_img(const SceneImpl &s, int id)
+{
+    if (id < 0 || id >= (int)s.images.size())
+        throw Error(PT_ERR_ARG, "bad image id " + std::to_string(id));
+}
+void check_tex(const SceneImpl &s, int id)
+{
+    if (id < 0 || id >= (int)s.textures.size())
+        throw Error(PT_ERR_ARG, "bad texture id " + std::to_string(id));
+}
+void check_mat(const SceneImpl &s, int id)
+{
+    if (id < 0 || id >= (int)s.materials.size())
+        throw Error(PT_ERR_ARG, "bad material id " + std::to_string(id));
+}
+void check_obj(const SceneImpl &s, int id)
+{
+    if (id < 0 || id >= (int)s.objects.size())
+        throw Error(PT_ERR_ARG, "bad object id " + std::to_string(id));
+}
+
+int add_tex(SceneImpl &s, const TexRec &t)
+{
+    s.textures.push_back(t);
+    return (int)s.textures.size() - 1;
+}
+
+int default_tex(SceneImpl &s, int which) /* ColorTexture(0) / ColorTexture(1) */
+{
+    TexRec t;
+    t.kind = TexKind::Color;
+    t.f[0] = t.f[1] = t.f[2] = (float)which;
+    return add_tex(s, t);
+}
+
+template <class F>
+int guard(F f)
+{
+    try {
+        return f();
+    } catch (Error &e) {
+        set_error(e.what());
+        return e.code;
+    } catch (std::exception &e) {
+        set_error(e.what());
+        return PT_ERR_ARG;
+    }
+}
+
+std::string trim(const std::string &s)
+{
+    size_t a = s.find_first_not_of(" \t\r"), b = s.find_last_not_of(" \t\r");
+    return a == std::string::npos ? "" : s.substr(a, b - a + 1);
+}
+
+float tof(const std::string &t)
+{
+    char *end = nullptr;
+    float v = strtof(t.c_str(), &end);
+    if (end == t.c_str() || *end)
+        throw Error(PT_ERR_ARG, "bad float '" + t + "'");
+    return v;
+}
+
+int toi(const std::string &t)
+{
+    char *end = nullptr;
+    long v = strtol(t.c_str(), &end, 10);
+    if (end == t.c_str() || *end)
+        throw Error(PT_ERR_ARG, "bad int '" + t + "'");
+    return (int)v;
+}
+
+/* Loads the plain-text scene format into s (ids are renumbered). */
+void load_text(SceneImpl &s, const std::string &text)
+{
+    s.clear();
+    std::map<int, int> img, tex, mat, obj;
+    std::istringstream in(text);
+    std::string line;
+    int root = -1;
+    auto need = [](const std::vector<std::string> &t, size_t n) {
+        if (t.size() != n)
+            throw Error(PT_ERR_ARG, "scene text: wrong operand count near '" + (t.empty() ? "" : t[0]) + "'");
+    };
+    auto look = [](std::map<int, int> &m, int id, const char *what) {
+        auto it = m.find(id);
+        if (it == m.end())
+            throw Error(PT_ERR_ARG, std::string("scene text: unknown ") + what + " " + std::to_string(id));
+        return it->second;
+    };
+    while (std::getline(in, line)) {
+        line = trim(line);
+        if (line.empty() || line[0] == '#')
+            continue;
+        std::istringstream ls(line);
+        std::vector<std::string> t;
+        std::string w;
+        while (ls >> w) t.push_back(w);
+        const std::string &k = t[0];
+        if (k == "root") {
+            need(t, 2);
+            root = look(obj, toi(t[1]), "object");
+            continue;
+        }
+        if (t.size() < 3)
+            throw Error(PT_ERR_ARG, "scene text: short line");
+        int id = toi(t[1]);
+        const std::string &ty = t[2];
+        if (k == "image") {
+            if (ty == "hdr") {
+                need(t, 4);
+                s.images.push_back(read_hdr(t[3]));
+            } else if (ty == "raw") {
+                need(t, 6);
+                ImageRec r;
+                r.w = toi(t[3]), r.h = toi(t[4]);
+                std::ifstream f(t[5], std::ios::binary);
+                if (!f)
+                    throw Error(PT_ERR_IO, "can't open " + t[5]);
+                r.rgba.resize((size_t)4 * r.w * r.h);
+                f.read((char *)r.rgba.data(), (std::streamsize)(r.rgba.size() * 4));
+                if (!f)
+                    throw Error(PT_ERR_IO, "short raw image " + t[5]);
+                s.images.push_back(std::move(r));
+            } else
+                throw Error(PT_ERR_ARG, "scene text: image kind " + ty);
+            img[id] = (int)s.images.size() - 1;
+        } else if (k == "tex") {
+            TexRec r;
+            if (ty == "color") {
+                need(t, 6);
+                r.kind = TexKind::Color;
+                for (int j = 0; j < 3; j++) r.f[j] = tof(t[3 + j]);
+            } else if (ty == "coord") {
+                need(t, 3);
+                r.kind = TexKind::Coord;
+            } else if (ty == "image" || ty == "image_alpha") {
+                need(t, 4);
+                r.kind = ty == "image" ? TexKind::Image : TexKind::ImageAlpha;
+                r.img[0] = look(img, toi(t[3]), "image");
+            } else if (ty == "skybox" || ty == "skybox_alpha") {
+                need(t, 9);
+                r.kind = ty == "skybox" ? TexKind::Skybox : TexKind::SkyboxAlpha;
+                for (int j = 0; j < 6; j++) r.img[j] = look(img, toi(t[3 + j]), "image");
+            } else if (ty == "multiply") {
+                need(t, 7);
+                r.kind = TexKind::Multiply;
+                for (int j = 0; j < 3; j++) r.f[j] = tof(t[3 + j]);
+                r.child = look(tex, toi(t[6]), "texture");
+            } else if (ty == "log" || ty == "mirrorball" || ty == "spherical") {
+                need(t, 4);
+                r.kind = ty == "log" ? TexKind::Log : ty == "mirrorball" ? TexKind::MirrorBall : TexKind::Spherical;
+                r.child = look(tex, toi(t[3]), "texture");
+            } else if (ty == "xform") {
+                need(t, 16);
+                r.kind = TexKind::Xform;
+                for (int j = 0; j < 12; j++) r.f[j] = tof(t[3 + j]);
+                r.child = look(tex, toi(t[15]), "texture");
+            } else
+                throw Error(PT_ERR_ARG, "scene text: texture kind " + ty);
+            tex[id] = add_tex(s, r);
+        } else if (k == "mat") {
+            need(t, 8);
+            MatRec m;
+            m.reflect = look(tex, toi(t[2]), "texture");
+            m.scatter = look(tex, toi(t[3]), "texture");
+            m.emissive = look(tex, toi(t[4]), "texture");
+            m.transmit = look(tex, toi(t[5]), "texture");
+            m.ior = tof(t[6]);
+            m.trc = look(tex, toi(t[7]), "texture");
+            s.materials.push_back(m);
+            mat[id] = (int)s.materials.size() - 1;
+        } else if (k == "obj") {
+            ObjRec o;
+            if (ty == "sphere" || ty == "plane") {
+                need(t, 8);
+                o.kind = ty == "sphere" ? ObjKind::Sphere : ObjKind::Plane;
+                for (int j = 0; j < 4; j++) o.f[j] = tof(t[3 + j]);
+                o.mat = look(mat, toi(t[7]), "material");
+            } else if (ty == "union" || ty == "intersection" || ty == "difference") {
+                need(t, 5);
+                o.kind = ty == "union" ? ObjKind::Union : ty == "intersection" ? ObjKind::Intersection
+                                                                                : ObjKind::Difference;
+                o.a = look(obj, toi(t[3]), "object");
+                o.b = look(obj, toi(t[4]), "object");
+            } else if (ty == "xform") {
+                need(t, 16);
+                o.kind = ObjKind::Xform;
+                for (int j = 0; j < 12; j++) o.f[j] = tof(t[3 + j]);
+                o.a = look(obj, toi(t[15]), "object");
+            } else
+                throw Error(PT_ERR_ARG, "scene text: object kind " + ty);
+            s.objects.push_back(o);
+            obj[id] = (int)s.objects.size() - 1;
+        } else
+            throw Error(PT_ERR_ARG, "scene text: unknown line kind " + k);
+    }
+    if (root < 0)
+        throw Error(PT_ERR_ARG, "scene text: no root");
+    s.root = root;
+}
+
+/* jump table (A_{3m}, G_{3m}), m = 0..64, of state_{n+3m} = A*state_n + G*inc */
+std::vector<uint64_t> jump_table()
+{
+    std::vector<uint64_t> t(2 * 65);
+    for (uint32_t m = 0; m <= 64; m++) pt_pcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
+    return t;
+}
+
+DeviceState &device_state(SceneImpl &s, int device, const Generated &g)
+{
+    HIPCHECK(hipSetDevice(device));
+    std::unique_ptr<DeviceState> &ds = s.devices[device];
+    if (!ds) {
+        ds.reset(new DeviceState);
+        ds->device = device;
+        std::vector<uint64_t> jt = jump_table();
+        ds->jump.ensure(jt.size());
+        HIPCHECK(hipMemcpy(ds->jump.p, jt.data(), jt.size() * 8, hipMemcpyHostToDevice));
+        ds->stats.ensure(16);
+    }
+    if (ds->key != g.key) {
+        const std::vector<char> &code = code_object(g);
+        if (ds->mod)
+            HIPCHECK(hipModuleUnload(ds->mod));
+        ds->mod = nullptr;
+        HIPCHECK(hipModuleLoadData(&ds->mod, code.data()));
+        HIPCHECK(hipModuleGetFunction(&ds->fast, ds->mod, "pt_render_fast"));
+        HIPCHECK(hipModuleGetFunction(&ds->strict, ds->mod, "pt_render_strict"));
+        HIPCHECK(hipModuleGetFunction(&ds->reduce, ds->mod, "pt_reduce"));
+        ds->key = g.key;
+    }
+    if (ds->params != g.params) {
+        ds->P.ensure(g.params.size());
+        HIPCHECK(hipMemcpy(ds->P.p, g.params.data(), g.params.size() * 4, hipMemcpyHostToDevice));
+        ds->params = g.params;
+    }
+    if (ds->img_ids != g.image_ids) {
+        for (auto &b : ds->img_data) b.release();
+        ds->img_data.clear();
+        ds->img_data.resize(g.image_ids.size());
+        std::vector<PtImageDev> desc(g.image_ids.size() + 1);
+        for (size_t k = 0; k < g.image_ids.size(); k++) {
+            const ImageRec &im = s.images.at(g.image_ids[k]);
+            ds->img_data[k].ensure(im.rgba.size());
+            HIPCHECK(hipMemcpy(ds->img_data[k].p, im.rgba.data(), im.rgba.size() * 4, hipMemcpyHostToDevice));
+            desc[k].data = ds->img_data[k].p;
+            desc[k].w = (uint32_t)im.w;
+            desc[k].h = (uint32_t)im.h;
+        }
+        ds->imgs.ensure(desc.size());
+        HIPCHECK(hipMemcpy(ds->imgs.p, desc.data(), desc.size() * sizeof(PtImageDev), hipMemcpyHostToDevice));
+        ds->img_ids = g.image_ids;
+    }
+    return *ds;
+}
+
+void validate(const pt_render_params *p)
+{
+    if (!p)
+        throw Error(PT_ERR_ARG, "null params");
+    if (p->width <= 0 || p->height <= 0 || p->spp <= 0)
+        throw Error(PT_ERR_ARG, "width, height and spp must be positive");
+    if ((int64_t)p->width * p->height >= (1ll << 31))
+        throw Error(PT_ERR_ARG, "frame too large");
+    if (p->spp >= (1 << 20))
+        throw Error(PT_ERR_ARG, "spp must be < 2^20 (engine key layout)");
+    if (p->depth < 0 || p->depth > 64)
+        throw Error(PT_ERR_ARG, "depth must be in [0, 64]");
+    if (p->order != PT_ORDER_GROUP64 && p->order != PT_ORDER_REFERENCE)
+        throw Error(PT_ERR_ARG, "bad order");
+    if (p->pixels) {
+        for (int64_t k = 0; k < p->npixels; k++)
+            if (p->pixels[k] < 0 || p->pixels[k] >= p->width * p->height)
+                throw Error(PT_ERR_ARG, "pixel index out of range");
+    }
+}
+
+void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream_t stream, pt_render_stats *st)
+{
+    validate(p);
+    Generated g = generate(s, p->depth);
+    s.last_key = g.key;
+    DeviceState &ds = device_state(s, p->device, g);
+    const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
+    if (npix == 0)
+        return;
+    const int *dpix = nullptr;
+    if (p->pixels) {
+        ds.pixels.ensure((size_t)npix);
+        HIPCHECK(hipMemcpyAsync(ds.pixels.p, p->pixels, (size_t)npix * 4, hipMemcpyHostToDevice, stream));
+        dpix = ds.pixels.p;
+    }
+    int64_t budget = p->max_buffer_bytes > 0 ? p->max_buffer_bytes : (8ll << 30);
+    long long per_pass = budget / (12ll * npix);
+    per_pass = per_pass / 64 * 64;
+    if (per_pass < 64)
+        per_pass = 64;
+    if (per_pass > p->spp)
+        per_pass = p->spp;
+    ds.stage.ensure((size_t)(npix * per_pass * 3));
+    if (p->spp > per_pass)
+        ds.accum.ensure((size_t)npix * 3);
+    if (st) {
+        memset(st, 0, sizeof(*st));
+        HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 16 * 8, stream));
+    }
+    hipFunction_t fn = p->order == PT_ORDER_REFERENCE ? ds.strict : ds.fast;
+    std::vector<hipEvent_t> evs;
+    auto event = [&]() {
+        hipEvent_t e;
+        HIPCHECK(hipEventCreate(&e));
+        HIPCHECK(hipEventRecord(e, stream));
+        evs.push_back(e);
+    };
+    std::vector<std::pair<int, int>> spans; /* (start event, end event) per render launch */
+    std::vector<std::pair<int, int>> rspans;
+    for (int s0 = 0; s0 < p->spp; s0 += (int)per_pass) {
+        int nsamp = (int)std::min<long long>(per_pass, p->spp - s0);
+        long long n_items = npix * nsamp;
+        long long chunks = (n_items + 63) / 64;
+        const long long max_grid = 1ll << 30;
+        for (long long c0 = 0; c0 < chunks; c0 += max_grid) {
+            long long nc = std::min(max_grid, chunks - c0);
+            PtLaunchHost lp;
+            memset(&lp, 0, sizeof lp);
+            lp.seed = p->seed;
+            lp.n_items = n_items;
+            lp.chunk0 = c0;
+            lp.W = p->width, lp.H = p->height;
+            lp.sw = p->screen_w, lp.sh = p->screen_h, lp.dist = p->screen_dist;
+            lp.depth = p->depth;
+            lp.nsamp = nsamp;
+            lp.s0 = s0;
+            const float *Pp = ds.P.p;
+            const PtImageDev *ip = ds.imgs.p;
+            const uint64_t *jp = ds.jump.p;
+            float *op = ds.stage.p;
+            const int *pp = dpix;
+            uint64_t *sp = st ? ds.stats.p : nullptr;
+            void *args[] = {&Pp, &ip, &jp, &op, &pp, &sp, &lp};
+            int e0 = (int)evs.size();
+            if (st)
+                event();
+            HIPCHECK(hipModuleLaunchKernel(fn, (unsigned)nc, 1, 1, 64, 1, 1, 0, stream, args, nullptr));
+            if (st) {
+                event();
+                spans.push_back({e0, e0 + 1});
+            }
+        }
+        {
+            const float *in = ds.stage.p;
+            float *acc = ds.accum.p;
+            const int *pp = dpix;
+            long long ns = npix;
+            int first = s0 == 0, last = s0 + nsamp == p->spp;
+            float spp = (float)p->spp;
+            void *args[] = {&in, &acc, &fb, &pp, &ns, &nsamp, &first, &last, &spp};
+            unsigned blocks = (unsigned)((npix + 255) / 256);
+            int e0 = (int)evs.size();
+            if (st)
+                event();
+            HIPCHECK(hipModuleLaunchKernel(ds.reduce, blocks, 1, 1, 256, 1, 1, 0, stream, args, nullptr));
+            if (st) {
+                event();
+                rspans.push_back({e0, e0 + 1});
+            }
+        }
+        if (st)
+            st->samples += (uint64_t)n_items;
+    }
+    if (st) {
+        HIPCHECK(hipStreamSynchronize(stream));
+        for (auto &sp : spans) {
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, evs[sp.first], evs[sp.second]));
+            st->kernel_ms += ms;
+            st->launches++;
+        }
+        for (auto &sp : rspans) {
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, evs[sp.first], evs[sp.second]));
+            st->reduce_ms += ms;
+        }
+        uint64_t c[16];
+        HIPCHECK(hipMemcpy(c, ds.stats.p, sizeof c, hipMemcpyDeviceToHost));
+        st->queries = c[0] + c[1];
+        st->leaf_queries = c[1];
+        st->attempts = c[2];
+        st->rounds = c[3];
+        st->sphere_tests = st->queries * (uint64_t)g.n_spheres;
+        st->plane_tests = st->queries * (uint64_t)g.n_planes;
+        for (auto e : evs) (void)hipEventDestroy(e);
+    }
+}
+
+} // namespace
+
+} // namespace pt
+
+using namespace pt;
+
+extern "C" {
+
+const char *pt_last_error(void) { return g_error.c_str(); }
+const char *pt_version(void) { return "pt-mi355x 0.1 (gfx950)"; }
+
+pt_scene *pt_scene_create(void) { return new pt_scene; }
+void pt_scene_destroy(pt_scene *s) { delete s; }
+
+pt_id pt_image_load_hdr(pt_scene *s, const char *path)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        sc.images.push_back(read_hdr(path ? path : ""));
+        return (int)sc.images.size() - 1;
+    });
+}
+
+pt_id pt_image_from_rgba32f(pt_scene *s, const float *rgba, int w, int h)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        if (!rgba || w <= 0 || h <= 0)
+            throw Error(PT_ERR_ARG, "bad image");
+        ImageRec r;
+        r.w = w, r.h = h;
+        r.rgba.assign(rgba, rgba + (size_t)4 * w * h);
+        sc.images.push_back(std::move(r));
+        return (int)sc.images.size() - 1;
+    });
+}
+
+int pt_hdr_read(const char *path, float *rgba, int *w, int *h)
+{
+    return guard([&] {
+        ImageRec r = read_hdr(path ? path : "");
+        if (w)
+            *w = r.w;
+        if (h)
+            *h = r.h;
+        if (rgba)
+            memcpy(rgba, r.rgba.data(), r.rgba.size() * 4);
+        return PT_OK;
+    });
+}
+
+pt_id pt_tex_color(pt_scene *s, float r, float g, float b)
+{
+    return guard([&] {
+        TexRec t;
+        t.kind = TexKind::Color;
+        t.f[0] = r, t.f[1] = g, t.f[2] = b;
+        return add_tex(S(s), t);
+    });
+}
+
+static pt_id tex_image(pt_scene *s, TexKind k, pt_id image)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        check_img(sc, image);
+        TexRec t;
+        t.kind = k;
+        t.img[0] = image;
+        return add_tex(sc, t);
+    });
+}
+pt_id pt_tex_image(pt_scene *s, pt_id image) { return tex_image(s, TexKind::Image, image); }
+pt_id pt_tex_image_alpha(pt_scene *s, pt_id image) { return tex_image(s, TexKind::ImageAlpha, image); }
+
+static pt_id tex_skybox(pt_scene *s, TexKind k, const pt_id *f)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        TexRec t;
+        t.kind = k;
+        for (int j = 0; j < 6; j++) {
+            check_img(sc, f[j]);
+            t.img[j] = f[j];
+        }
+        return add_tex(sc, t);
+    });
+}
+pt_id pt_tex_skybox(pt_scene *s, pt_id top, pt_id bottom, pt_id left, pt_id right, pt_id front, pt_id back)
+{
+    pt_id f[6] = {top, bottom, left, right, front, back};
+    return tex_skybox(s, TexKind::Skybox, f);
+}
+pt_id pt_tex_skybox_alpha(pt_scene *s, pt_id top, pt_id bottom, pt_id left, pt_id right, pt_id front, pt_id back)
+{
+    pt_id f[6] = {top, bottom, left, right, front, back};
+    return tex_skybox(s, TexKind::SkyboxAlpha, f);
+}
+
+static pt_id tex_wrap(pt_scene *s, TexKind k, pt_id inner, const float *f, int nf)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        check_tex(sc, inner);
+        TexRec t;
+        t.kind = k;
+        t.child = inner;
+        for (int j = 0; j < nf; j++) t.f[j] = f[j];
+        return add_tex(sc, t);
+    });
+}
+pt_id pt_tex_multiply(pt_scene *s, float r, float g, float b, pt_id t)
+{
+    float f[3] = {r, g, b};
+    return tex_wrap(s, TexKind::Multiply, t, f, 3);
+}
+pt_id pt_tex_log(pt_scene *s, pt_id t) { return tex_wrap(s, TexKind::Log, t, nullptr, 0); }
+pt_id pt_tex_mirrorball(pt_scene *s, pt_id t) { return tex_wrap(s, TexKind::MirrorBall, t, nullptr, 0); }
+pt_id pt_tex_spherical(pt_scene *s, pt_id t) { return tex_wrap(s, TexKind::Spherical, t, nullptr, 0); }
+pt_id pt_tex_transformed(pt_scene *s, const float m[12], pt_id t)
+{
+    if (!m) {
+        set_error("null matrix");
+        return PT_ERR_ARG;
+    }
+    return tex_wrap(s, TexKind::Xform, t, m, 12);
+}
+pt_id pt_tex_coord(pt_scene *s)
+{
+    return guard([&] {
+        TexRec t;
+        t.kind = TexKind::Coord;
+        return add_tex(S(s), t);
+    });
+}
+
+pt_id pt_material(pt_scene *s, pt_id reflect, pt_id scatter, pt_id emissive, pt_id transmit, float ior,
+                  pt_id transmit_reflect)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        /* include/material.h:18 defaults: reflect 1, scatter 1, emissive 0, transmit 0, trc 0 */
+        if (reflect < 0)
+            reflect = default_tex(sc, 1);
+        if (scatter < 0)
+            scatter = default_tex(sc, 1);
+        if (emissive < 0)
+            emissive = default_tex(sc, 0);
+        if (transmit < 0)
+            transmit = default_tex(sc, 0);
+        if (transmit_reflect < 0)
+            transmit_reflect = default_tex(sc, 0);
+        for (int t : {reflect, scatter, emissive, transmit, transmit_reflect}) check_tex(sc, t);
+        MatRec m{reflect, scatter, emissive, transmit, transmit_reflect, ior};
+        sc.materials.push_back(m);
+        return (int)sc.materials.size() - 1;
+    });
+}
+
+pt_id pt_sphere(pt_scene *s, float cx, float cy, float cz, float r, pt_id mat)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        check_mat(sc, mat);
+        ObjRec o;
+        o.kind = ObjKind::Sphere;
+        o.f[0] = cx, o.f[1] = cy, o.f[2] = cz, o.f[3] = r;
+        o.mat = mat;
+        sc.objects.push_back(o);
+        return (int)sc.objects.size() - 1;
+    });
+}
+
+pt_id pt_plane(pt_scene *s, float nx, float ny, float nz, float d, pt_id mat)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        check_mat(sc, mat);
+        ObjRec o;
+        o.kind = ObjKind::Plane;
+        o.f[0] = nx, o.f[1] = ny, o.f[2] = nz, o.f[3] = d;
+        o.mat = mat;
+        sc.objects.push_back(o);
+        return (int)sc.objects.size() - 1;
+    });
+}
+
+pt_id pt_plane_through(pt_scene *s, float nx, float ny, float nz, float px, float py, float pz, pt_id mat)
+{
+    /* Plane(normal, pos): d = -dot(normal, pos), src/plane.cpp:11-14 */
+    float d = -((nx * px + ny * py) + nz * pz);
+    return pt_plane(s, nx, ny, nz, d, mat);
+}
+
+pt_id pt_csg(pt_scene *s, int op, pt_id a, pt_id b)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        check_obj(sc, a);
+        check_obj(sc, b);
+        ObjRec o;
+        if (op == PT_CSG_UNION)
+            o.kind = ObjKind::Union;
+        else if (op == PT_CSG_INTERSECTION)
+            o.kind = ObjKind::Intersection;
+        else if (op == PT_CSG_DIFFERENCE)
+            o.kind = ObjKind::Difference;
+        else
+            throw Error(PT_ERR_ARG, "bad csg op");
+        o.a = a, o.b = b;
+        sc.objects.push_back(o);
+        return (int)sc.objects.size() - 1;
+    });
+}
+
+pt_id pt_transformed(pt_scene *s, const float m[12], pt_id child)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        if (!m)
+            throw Error(PT_ERR_ARG, "null matrix");
+        check_obj(sc, child);
+        float inv[12];
+        mat_inverse(m, inv); /* the reference inverts in the iterator ctor and throws there */
+        ObjRec o;
+        o.kind = ObjKind::Xform;
+        memcpy(o.f, m, 48);
+        o.a = child;
+        sc.objects.push_back(o);
+        return (int)sc.objects.size() - 1;
+    });
+}
+
+int pt_set_root(pt_scene *s, pt_id obj)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        check_obj(sc, obj);
+        sc.root = obj;
+        return PT_OK;
+    });
+}
+
+int pt_scene_from_text(pt_scene *s, const char *text)
+{
+    return guard([&] {
+        load_text(S(s), text ? text : "");
+        return PT_OK;
+    });
+}
+
+void pt_matrix_rotate(const float axis[3], double angle, float out[12]) { mat_rotate(axis, angle, out); }
+int pt_matrix_inverse(const float m[12], float out[12])
+{
+    return guard([&] {
+        mat_inverse(m, out);
+        return PT_OK;
+    });
+}
+void pt_matrix_concat(const float a[12], const float b[12], float out[12]) { mat_concat(a, b, out); }
+
+int pt_scene_compile(pt_scene *s, int depth)
+{
+    return guard([&] {
+        Generated g = generate(S(s), depth);
+        code_object(g);
+        S(s).last_key = g.key;
+        return PT_OK;
+    });
+}
+
+const char *pt_scene_kernel_key(pt_scene *s, int depth)
+{
+    thread_local std::string k;
+    try {
+        k = generate(S(s), depth).key;
+    } catch (std::exception &e) {
+        set_error(e.what());
+        k.clear();
+    }
+    return k.c_str();
+}
+
+int pt_render_device(pt_scene *s, const pt_render_params *p, float *fb, void *stream, pt_render_stats *stats)
+{
+    return guard([&] {
+        if (!fb)
+            throw Error(PT_ERR_ARG, "null frame buffer");
+        render_device(S(s), p, fb, (hipStream_t)stream, stats);
+        return PT_OK;
+    });
+}
+
+int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_stats *stats)
+{
+    return guard([&] {
+        if (!rgb_out)
+            throw Error(PT_ERR_ARG, "null output");
+        validate(p);
+        SceneImpl &sc = S(s);
+        HIPCHECK(hipSetDevice(p->device));
+        size_t n = (size_t)p->width * p->height * 3;
+        DevBuf<float> fb;
+        fb.ensure(n);
+        struct Free
+        {
+            DevBuf<float> &b;
+            ~Free() { b.release(); }
+        } fr{fb};
+        HIPCHECK(hipMemset(fb.p, 0, n * 4));
+        pt_render_stats local;
+        render_device(sc, p, fb.p, nullptr, stats ? stats : &local);
+        HIPCHECK(hipDeviceSynchronize());
+        if (!p->pixels) {
+            HIPCHECK(hipMemcpy(rgb_out, fb.p, n * 4, hipMemcpyDeviceToHost));
+        } else {
+            std::vector<float> all(n);
+            HIPCHECK(hipMemcpy(all.data(), fb.p, n * 4, hipMemcpyDeviceToHost));
+            for (int64_t k = 0; k < p->npixels; k++)
+                for (int c = 0; c < 3; c++) rgb_out[3 * k + c] = all[3 * (size_t)p->pixels[k] + c];
+        }
+        return PT_OK;
+    });
+}
+
+int pt_write_hdr(const char *path, const float *rgb, int w, int h)
+{
+    return guard([&] {
+        if (!path || !rgb || w <= 0 || h <= 0)
+            throw Error(PT_ERR_ARG, "bad arguments");
+        write_hdr(path, rgb, w, h);
+        return PT_OK;
+    });
+}
+
+int pt_write_bmp(const char *path, const float *rgb, int w, int h, int count)
+{
+    return guard([&] {
+        if (!path || !rgb || w <= 0 || h <= 0 || count <= 0)
+            throw Error(PT_ERR_ARG, "bad arguments");
+        write_bmp(path, rgb, w, h, count);
+        return PT_OK;
+    });
+}
+
+} // extern "C"

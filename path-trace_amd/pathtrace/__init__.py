@@ -1,0 +1,165 @@
+"""pathtrace -- MI355X-native renderer for the reference's per-pixel
+Monte-Carlo path (tracePixel -> traceRay -> CSG span queries -> shading).
+
+Python mirror of the reference's scene API (pathtrace.scene) on top of the
+C-ABI library libpt.so (include/pt/pt.h), whose megakernel runs on gfx950.
+
+    from pathtrace import *
+    world = Union(Sphere((0, 0, -4), .5, Material(ColorTexture(.8), ColorTexture(1))),
+                  Plane((0, 1, 0), .5, Material(ColorTexture(0), ColorTexture(0), ColorTexture(2))))
+    img = render(world, 256, 256, spp=16, depth=4)        # H x W x 3 float32 (tracePixel means)
+    write_hdr("out.hdr", img); write_bmp("out.bmp", img)
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import PT_ORDER_GROUP64, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, load_hdr, \
+    write_bmp, write_hdr
+from .scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTexture, ImageSkyboxAlphaTexture,
+                    ImageSkyboxTexture, ImageTexture, Intersection, LogTexture, Material, Matrix,
+                    MirrorBallSkymapTexture, MultiplyTexture, Object, Plane, SphericalCoordinatesSkymapTexture,
+                    Sphere, Texture, TransformedObject, TransformedTexture, Union, invert, to_text,
+                    transform_material, transform_object, transform_texture, union_array)
+
+__all__ = [n for n in dir() if not n.startswith("_")] + ["DeviceScene", "render", "render_device"]
+
+ORDERS = {"fast": PT_ORDER_GROUP64, "group64": PT_ORDER_GROUP64, "reference": PT_ORDER_REFERENCE,
+          "strict": PT_ORDER_REFERENCE}
+
+
+class DeviceScene:
+    """A pt_scene built from a Python scene graph through the C-ABI
+    constructors (one pt_* call per reference constructor)."""
+
+    def __init__(self, root: Object):
+        L = _lib.lib()
+        self._h = L.pt_scene_create()
+        if not self._h:
+            raise PtError("pt_scene_create failed")
+        self._img = {}
+        self._mat = {}
+        self.root = root
+        _lib.check(L.pt_set_root(self._h, self._obj(root)))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            _lib.lib().pt_scene_destroy(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _image(self, im: Image) -> int:
+        k = id(im)
+        if k not in self._img:
+            d = np.ascontiguousarray(im.data, dtype=np.float32)
+            self._img[k] = _lib.check(_lib.lib().pt_image_from_rgba32f(self._h, d.ctypes.data, d.shape[1],
+                                                                       d.shape[0]))
+        return self._img[k]
+
+    def _tex(self, t: Texture) -> int:
+        L, h, c = _lib.lib(), self._h, _lib.check
+        if isinstance(t, ColorTexture):
+            return c(L.pt_tex_color(h, *[float(v) for v in t.color]))
+        if isinstance(t, CoordTexture):
+            return c(L.pt_tex_coord(h))
+        if isinstance(t, ImageSkyboxAlphaTexture):
+            return c(L.pt_tex_skybox_alpha(h, *[self._image(f) for f in t.faces]))
+        if isinstance(t, ImageSkyboxTexture):
+            return c(L.pt_tex_skybox(h, *[self._image(f) for f in t.faces]))
+        if isinstance(t, ImageAlphaTexture):
+            return c(L.pt_tex_image_alpha(h, self._image(t.image)))
+        if isinstance(t, ImageTexture):
+            return c(L.pt_tex_image(h, self._image(t.image)))
+        if isinstance(t, MultiplyTexture):
+            inner = self._tex(t.t)
+            return c(L.pt_tex_multiply(h, *[float(v) for v in t.factor], inner))
+        if isinstance(t, TransformedTexture):
+            inner = self._tex(t.t)
+            return c(L.pt_tex_transformed(h, _lib._f12(t.matrix.m), inner))
+        if isinstance(t, MirrorBallSkymapTexture):
+            return c(L.pt_tex_mirrorball(h, self._tex(t.t)))
+        if isinstance(t, SphericalCoordinatesSkymapTexture):
+            return c(L.pt_tex_spherical(h, self._tex(t.t)))
+        if isinstance(t, LogTexture):
+            return c(L.pt_tex_log(h, self._tex(t.t)))
+        raise TypeError("unsupported texture %r" % (t,))
+
+    def _material(self, m: Material) -> int:
+        k = id(m)
+        if k not in self._mat:
+            ids = [self._tex(t) for t in m.textures()]
+            self._mat[k] = _lib.check(_lib.lib().pt_material(self._h, ids[0], ids[1], ids[2], ids[3],
+                                                              float(m.ior), ids[4]))
+        return self._mat[k]
+
+    def _obj(self, o: Object) -> int:
+        L, h, c = _lib.lib(), self._h, _lib.check
+        if isinstance(o, Sphere):
+            return c(L.pt_sphere(h, *[float(v) for v in o.center], float(o.r), self._material(o.material)))
+        if isinstance(o, Plane):
+            return c(L.pt_plane(h, *[float(v) for v in o.normal], float(o.d), self._material(o.material)))
+        if isinstance(o, (Union, Intersection, Difference)):
+            op = {Union: 0, Intersection: 1, Difference: 2}[type(o)]
+            a = self._obj(o.a)
+            b = self._obj(o.b)
+            return c(L.pt_csg(h, op, a, b))
+        if isinstance(o, TransformedObject):
+            ch = self._obj(o.o)
+            return c(L.pt_transformed(h, _lib._f12(o.matrix.m), ch))
+        raise TypeError("unsupported object %r" % (o,))
+
+    def compile(self, depth: int) -> str:
+        _lib.check(_lib.lib().pt_scene_compile(self._h, depth))
+        return _lib.lib().pt_scene_kernel_key(self._h, depth).decode()
+
+
+def make_params(width, height, spp, depth, screen=None, seed=0x5EED, order="fast", device=0, pixels=None,
+                max_buffer_bytes=0):
+    sw, sh, dist = screen if screen is not None else (float(width), float(height), float(2 * min(width, height)))
+    p = RenderParams()
+    p.width, p.height, p.spp, p.depth = int(width), int(height), int(spp), int(depth)
+    p.screen_w, p.screen_h, p.screen_dist = float(sw), float(sh), float(dist)
+    p.seed = int(seed)
+    p.order = ORDERS[order] if isinstance(order, str) else int(order)
+    p.device = int(device)
+    keep = None
+    if pixels is not None:
+        keep = np.ascontiguousarray(np.asarray(pixels, dtype=np.int32))
+        p.pixels = keep.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        p.npixels = len(keep)
+    else:
+        p.pixels = None
+        p.npixels = 0
+    p.max_buffer_bytes = int(max_buffer_bytes)
+    return p, keep
+
+
+def render(scene, width: int, height: int, spp: int, depth: int, screen=None, seed: int = 0x5EED,
+           order="fast", pixels: Optional[Sequence[int]] = None, device: int = 0, stats: bool = False,
+           max_buffer_bytes: int = 0):
+    """tracePixel means for every pixel (H x W x 3), or for `pixels` (n x 3)."""
+    ds = scene if isinstance(scene, DeviceScene) else DeviceScene(scene)
+    p, keep = make_params(width, height, spp, depth, screen, seed, order, device, pixels, max_buffer_bytes)
+    n = (len(keep) if keep is not None else width * height)
+    out = np.zeros((n, 3), dtype=np.float32)
+    st = RenderStats()
+    _lib.check(_lib.lib().pt_render(ds.handle, ctypes.byref(p), out.ctypes.data, ctypes.byref(st)))
+    if keep is None:
+        out = out.reshape(height, width, 3)
+    return (out, st.as_dict()) if stats else out
+
+
+def render_device(scene: DeviceScene, params: RenderParams, fb_ptr: int, stream_ptr: int = 0, stats: bool = False):
+    """Render into device memory fb_ptr (W*H*3 floats) on stream_ptr."""
+    st = RenderStats()
+    _lib.check(_lib.lib().pt_render_device(scene.handle, ctypes.byref(params), ctypes.c_void_p(fb_ptr),
+                                           ctypes.c_void_p(stream_ptr), ctypes.byref(st) if stats else None))
+    return st.as_dict() if stats else None
