@@ -7,6 +7,7 @@
  * turn into straight-line, fully inlined code per scene.
  */
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <sstream>
@@ -207,6 +208,15 @@ Generated generate(const SceneImpl &s, int depth)
     while (maxd < depth) maxd *= 2;
 
     std::ostringstream src;
+    /* experiment hook: extra preprocessor definitions, e.g. PT_DEVICE_DEFINES="PT_LEAF_STUB=1" */
+    if (const char *defs = getenv("PT_DEVICE_DEFINES")) {
+        std::istringstream ds(defs);
+        std::string d;
+        while (ds >> d) {
+            size_t eq = d.find('=');
+            src << "#define " << (eq == std::string::npos ? d : d.substr(0, eq) + " " + d.substr(eq + 1)) << "\n";
+        }
+    }
     src << device_library_source() << "\n";
     src << "namespace ptgen {\nusing namespace ptd;\n";
     src << "typedef " << root << " RootT;\n";

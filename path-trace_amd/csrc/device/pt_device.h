@@ -357,6 +357,10 @@ struct Pln
         return B::normal(prim, t, o, d, e);                                                         \
     }
 
+/* Each merge step decides what to emit and which child to advance, then
+ * advances each child at exactly ONE call site: the inlined code of a CSG
+ * tree stays linear in its node count instead of multiplying per level. */
+
 /* src/union.cpp:84-134 */
 template <class A, class B>
 struct Uni
@@ -365,37 +369,32 @@ struct Uni
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
         for (;;) {
+            if (s.ea && s.eb)
+                return false;
+            bool emit = true, adv_a = false;
             if (s.ea) {
-                if (s.eb)
-                    return false;
                 out = s.sb;
-                s.eb = !B::pull(s.b, s.sb);
-                return true;
-            }
-            if (s.eb) {
-                out = s.sa;
-                s.ea = !A::pull(s.a, s.sa);
-                return true;
-            }
-            if (s.sa.t1 < s.sb.t0) {
-                out = s.sa;
-                s.ea = !A::pull(s.a, s.sa);
-                return true;
-            }
-            if (s.sb.t1 < s.sa.t0) {
+            } else if (s.eb) {
+                out = s.sa, adv_a = true;
+            } else if (s.sa.t1 < s.sb.t0) {
+                out = s.sa, adv_a = true;
+            } else if (s.sb.t1 < s.sa.t0) {
                 out = s.sb;
-                s.eb = !B::pull(s.b, s.sb);
-                return true;
-            }
-            if (s.sa.t0 < s.sb.t0) {
+            } else if (s.sa.t0 < s.sb.t0) {
                 if (s.sa.t1 < s.sb.t1)
                     end_from_end(s.sa, s.sb);
-                s.eb = !B::pull(s.b, s.sb);
+                emit = false;
             } else {
                 if (s.sa.t1 > s.sb.t1)
                     end_from_end(s.sb, s.sa);
-                s.ea = !A::pull(s.a, s.sa);
+                emit = false, adv_a = true;
             }
+            if (adv_a)
+                s.ea = !A::pull(s.a, s.sa);
+            else
+                s.eb = !B::pull(s.b, s.sb);
+            if (emit)
+                return true;
         }
     }
 };
@@ -410,34 +409,30 @@ struct Isect
         for (;;) {
             if (s.ea || s.eb)
                 return false;
+            bool emit = true, adv_a;
             if (s.sa.t1 < s.sb.t0) {
-                s.ea = !A::pull(s.a, s.sa);
-                continue;
-            }
-            if (s.sb.t1 < s.sa.t0) {
-                s.eb = !B::pull(s.b, s.sb);
-                continue;
-            }
-            if (s.sa.t0 < s.sb.t0) {
+                emit = false, adv_a = true;
+            } else if (s.sb.t1 < s.sa.t0) {
+                emit = false, adv_a = false;
+            } else if (s.sa.t0 < s.sb.t0) {
                 if (s.sa.t1 < s.sb.t1) {
                     start_from_start(s.sa, s.sb);
-                    out = s.sa;
-                    s.ea = !A::pull(s.a, s.sa);
-                    return true;
+                    out = s.sa, adv_a = true;
+                } else {
+                    out = s.sb, adv_a = false;
                 }
-                out = s.sb;
-                s.eb = !B::pull(s.b, s.sb);
-                return true;
-            }
-            if (s.sb.t1 < s.sa.t1) {
+            } else if (s.sb.t1 < s.sa.t1) {
                 start_from_start(s.sb, s.sa);
-                out = s.sb;
-                s.eb = !B::pull(s.b, s.sb);
-                return true;
+                out = s.sb, adv_a = false;
+            } else {
+                out = s.sa, adv_a = true;
             }
-            out = s.sa;
-            s.ea = !A::pull(s.a, s.sa);
-            return true;
+            if (adv_a)
+                s.ea = !A::pull(s.a, s.sa);
+            else
+                s.eb = !B::pull(s.b, s.sb);
+            if (emit)
+                return true;
         }
     }
 };
@@ -452,38 +447,35 @@ struct Diff
         for (;;) {
             if (s.ea)
                 return false;
+            bool emit = true, adv_a = true;
             if (s.eb) {
                 out = s.sa;
-                s.ea = !A::pull(s.a, s.sa);
-                return true;
-            }
-            if (s.sa.t1 < s.sb.t0) {
+            } else if (s.sa.t1 < s.sb.t0) {
                 out = s.sa;
-                s.ea = !A::pull(s.a, s.sa);
-                return true;
-            }
-            if (s.sb.t1 < s.sa.t0) {
-                s.eb = !B::pull(s.b, s.sb);
+            } else if (s.sb.t1 < s.sa.t0) {
+                emit = false, adv_a = false;
             } else if (s.sa.t0 < s.sb.t0) {
                 if (s.sa.t1 < s.sb.t1) {
                     end_from_start(s.sa, s.sb);
                     out = s.sa;
-                    s.ea = !A::pull(s.a, s.sa);
-                    return true;
+                } else {
+                    out = s.sa;
+                    end_from_start(out, s.sb);
+                    start_from_end(s.sa, s.sb);
+                    adv_a = false;
                 }
-                out = s.sa;
-                end_from_start(out, s.sb);
-                start_from_end(s.sa, s.sb);
-                s.eb = !B::pull(s.b, s.sb);
-                return true;
+            } else if (s.sa.t1 > s.sb.t1) {
+                end_from_start(s.sa, s.sb);
+                emit = false, adv_a = false;
             } else {
-                if (s.sa.t1 > s.sb.t1) {
-                    end_from_start(s.sa, s.sb);
-                    s.eb = !B::pull(s.b, s.sb);
-                    continue;
-                }
-                s.ea = !A::pull(s.a, s.sa);
+                emit = false;
             }
+            if (adv_a)
+                s.ea = !A::pull(s.a, s.sa);
+            else
+                s.eb = !B::pull(s.b, s.sb);
+            if (emit)
+                return true;
         }
     }
 };
@@ -908,8 +900,24 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
                 u32 ref;
                 bool ex;
                 V3 col = mk(0, 0, 0);
+#if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
+                /* experiment: generation cost only */
+                if (dir.z < 0.0f) {
+                    t = 1.0f, ref = 0u;
+                    col = S::emis(0, hit + t * dir, e);
+                }
+#elif defined(PT_LEAF_STUB) && PT_LEAF_STUB == 2
+                /* experiment: primitive tests without CSG merges */
+                {
+                    typename S::Root::St st;
+                    S::Root::init(st, ctx, dir, dot(dir, dir), e);
+                    t = st.sa.t0 + st.sb.t0;
+                    col = S::emis(0, hit + t * dir, e);
+                }
+#else
                 if (first_hit<typename S::Root>(ctx, dir, e, t, ref, ex))
                     col = S::emis(ref_mat(ref), hit + t * dir, e);
+#endif
                 term = ((aN * en.w) * rc) * col;
             }
             if (STRICT) {
@@ -1126,12 +1134,16 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
 
 } // namespace ptd
 
+#ifndef PT_MIN_WAVES
+#define PT_MIN_WAVES 1
+#endif
+
 #define PT_RENDER_ARGS                                                                                     \
     const float *__restrict__ P, const ptd::PtImage *__restrict__ imgs, const u64 *__restrict__ jump,      \
         float *__restrict__ out, const int *__restrict__ pixels, u64 *__restrict__ stats, ptd::PtLaunch lp
 
 #define PT_DEFINE_KERNELS(SCENE, MAXD)                                                                      \
-    extern "C" __global__ __launch_bounds__(64) void pt_render_fast(PT_RENDER_ARGS)                         \
+    extern "C" __global__ __launch_bounds__(64, PT_MIN_WAVES) void pt_render_fast(PT_RENDER_ARGS)           \
     {                                                                                                       \
         ptd::render_chunk<SCENE, MAXD, false>(P, imgs, jump, out, pixels, stats, lp);                      \
     }                                                                                                       \
