@@ -1,0 +1,172 @@
+"""bench.py -- BASELINE.json's headline metric on MI355X:
+Msamples/s at 1920x1080x1024spp (config C3: 6-sphere union/difference CSG +
+sky wall, depth 8), with the per-channel RMSE of the GPU frame against the
+reference CPU renderer on a hashed pixel subset.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
+
+One step = one full frame: every rank renders the 16x16 tiles it owns
+(pathtrace.dist) into a zeroed full-frame float3 buffer with the HIP
+megakernel (libpt.so, C ABI) and the frames are sum-reduced to rank 0 over
+RCCL; the timed region is bracketed by barrier + device synchronise and the
+max over ranks is reported.  Inputs (the scene) are resident before timing.
+
+Extra fields: `roofline` (VALU-bound: the SURVEY.md s8(d) FP32 op model per
+root query x the kernel's exact query count / HIP-event kernel time, against
+78.6 T non-FMA FP32 op/s) and `cpu_baseline` (the unmodified reference sources,
+oracle/_ref/ptref, on the GPU box's host cores over a bounded pixel sample of
+the same frame, rank 0 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "path-trace_amd"), os.path.join(ROOT, "oracle")]
+
+VALU_PEAK_TOPS = 78.6  # 256 CU x 128 FP32 lanes/clk x 2.4 GHz, no FMA (contraction off for parity)
+# SURVEY.md s8(d) op model calibrated by tools/calibrate_ops.py C3 8192 32 (oracle event counts)
+OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=0)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--spp", type=int, default=0, help="override (for quick local probes only; invalid metric)")
+    ap.add_argument("--cpu-pixels", type=int, default=512)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--order", default="fast")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, txt, spp, npix, threads):
+    """The reference's own hot path on host cores over a hashed pixel subset."""
+    import oracle_py as O
+    rng = np.random.default_rng(0x5EED)
+    pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
+    if O.ref_available():
+        kind = "reference"
+        res, info = O.ref_render(txt, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, pixels=pix,
+                                 threads=threads, info=True)
+        secs = info["seconds"]
+    else:  # restated oracle (same arithmetic, pinned to the reference by tests/golden)
+        kind = "port"
+        t0 = time.time()
+        res = O.render(txt, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, pixels=pix, threads=threads)
+        secs = time.time() - t0
+    return pix, res, {"value": npix * spp / secs / 1e6, "unit": "Msamples/s", "cores": threads, "kind": kind,
+                      "sample": "%d hashed pixels x %d spp of the same frame (%.1f s)" % (npix, spp, secs)}
+
+
+def main():
+    args = parse()
+    import torch
+    import pathtrace as pt
+    from pathtrace import dist as ptdist
+    from pathtrace import scenes
+    from pathtrace.scene import to_text
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(local)
+
+    cfg = scenes.CONFIGS[args.config]
+    spp = args.spp or cfg.spp
+    W, H = cfg.width, cfg.height
+    root = cfg.scene()
+    ds = pt.DeviceScene(root)
+    mine = ptdist.rank_pixels(W, H, rank, world)
+    fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    params, keep = pt.make_params(W, H, spp, cfg.depth, screen=cfg.screen, order=args.order, device=local,
+                                  pixels=None if world == 1 else mine, max_buffer_bytes=40 << 30)
+    # untimed: load the code object, upload the scene, allocate every buffer
+    pt.prepare(ds, params)
+    torch.cuda.synchronize()
+
+    def step():
+        fb.zero_()
+        st = pt.render_device(ds, params, fb.data_ptr(), stream.cuda_stream, stats=True)
+        if dist is not None:
+            dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(s["kernel_ms"] for s in stats) / max(1, sum(s["launches"] for s in stats))
+    launches_per_step = stats[0]["launches"]
+    queries = sum(s["queries"] for s in stats)
+    if dist is not None:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+        q = torch.tensor([queries], dtype=torch.float64, device="cuda")
+        dist.all_reduce(q, op=dist.ReduceOp.SUM)
+        queries = int(q[0])
+
+    if rank == 0:
+        samples = W * H * spp * args.steps
+        value = samples / elapsed / 1e6
+        frame = fb.view(H, W, 3).cpu().numpy()
+        out = {
+            "metric": "Msamples/sec at 1920x1080x1024spp; per-channel RMSE vs CPU ref",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "%s: %dx%d, %d spp, depth %d, %s" % (cfg.name, W, H, spp, cfg.depth, cfg.note),
+                       "order": args.order, "sharding": "16x16 tiles hashed over ranks + RCCL reduce"},
+            "queries_per_sample": round(queries / samples, 2),
+        }
+        opq = OPS_PER_QUERY.get(cfg.name)
+        if opq:
+            ops_per_launch = opq * queries / (args.steps * launches_per_step * world)
+            achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12
+            out["roofline"] = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS,
+                               "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+                               "kernel": "pt_render_fast", "avg_launch_ms": round(kernel_ms, 2),
+                               "ops_per_query": opq}
+        if not args.no_cpu and world == 1:
+            try:
+                pix, ref, cb = cpu_baseline(cfg, to_text(root, "/tmp/pt_bench_img"), spp, args.cpu_pixels,
+                                            args.cpu_threads)
+                gpu = frame.reshape(-1, 3)[pix]
+                out["rmse_vs_cpu_ref"] = [float(v) for v in
+                                          np.sqrt(np.mean((gpu.astype(np.float64) - ref) ** 2, axis=0))]
+                out["cpu_baseline"] = cb
+            except Exception as e:  # report, never hide
+                out["cpu_baseline"] = {"error": str(e)[:300]}
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -143,12 +143,22 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
  * enqueued... or completed when stats != NULL (stats need the timings). */
 int pt_render_device(pt_scene *s, const pt_render_params *p, float *fb, void *stream, pt_render_stats *stats);
 
+/* Everything a render with p needs -- code object loaded, scene parameters
+ * and images uploaded, staging buffers allocated -- without rendering, so a
+ * timed or latency-sensitive render does no compilation or allocation. */
+int pt_prepare(pt_scene *s, const pt_render_params *p);
+
 /* JIT-compile (or fetch from the code-object cache) the megakernel for this
  * scene and depth without touching a GPU.  Used by build() to pre-populate the
  * in-tree cache. */
 int pt_scene_compile(pt_scene *s, int depth);
 /* Key of the code object for this scene/depth (hex string, static storage). */
 const char *pt_scene_kernel_key(pt_scene *s, int depth);
+
+/* Device self-test: the megakernel's exact fast paths for f32 sqrt / '/' /
+ * normalize against the compiler's correctly rounded ones on n hashed inputs.
+ * mismatches[0..2] receive the sqrt, div and normalize mismatch counts. */
+int pt_selftest_math(int device, uint64_t n, uint64_t seed, uint64_t *mismatches);
 
 /* ------------------------------------------------------------- output --- */
 /* MutableImage::writeHDR (reference src/image.cpp:398-481), rgb = w*h*3 floats. */

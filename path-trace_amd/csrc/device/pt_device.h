@@ -98,6 +98,82 @@ __device__ __forceinline__ V3 normalize(V3 v)
         m = 1.0f;
     return v / m;
 }
+/* Exact fast paths for f32 sqrt and '/'.  LLVM lowers correctly rounded
+ * sqrtf and '/' on gfx950 to fixed sequences (v_sqrt + ulp fix-up with
+ * range scaling and a class check; v_div_scale / v_rcp / 5 FMAs /
+ * v_div_fmas / v_div_fixup).  For operands in the ranges below the scaling
+ * steps are the identity, so the remaining core -- copied instruction for
+ * instruction -- returns the same bits; other operands take the full path.
+ * pt_selftest_math() checks this on the GPU against the compiler's own
+ * sqrtf and '/'. */
+__device__ __forceinline__ float sqrt_core(float x)
+{
+    float s = __builtin_amdgcn_sqrtf(x);
+    float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+    s = (rd <= 0.0f) ? sd : s;
+    s = (ru > 0.0f) ? su : s;
+    return s;
+}
+__device__ __forceinline__ float csqrt(float x) /* == __builtin_sqrtf(x), bitwise */
+{
+    float s = sqrt_core(x);
+    if (!(x >= 0x1p-96f && x <= 0x1.fffffep127f))
+        s = __builtin_sqrtf(x);
+    return s;
+}
+struct Rcp /* refined reciprocal of a denominator, shared by several quotients */
+{
+    float d, r;
+};
+__device__ __forceinline__ Rcp mkrcp(float d)
+{
+    Rcp R;
+    R.d = d;
+    float r = __builtin_amdgcn_rcpf(d);
+    float e = __builtin_fmaf(-d, r, 1.0f);
+    R.r = __builtin_fmaf(e, r, r);
+    return R;
+}
+/* |x| in [2^-30, 2^30] for denominators, [2^-60, 2^60] for numerators: no
+ * v_div_scale scaling (exponent gap < 96, no denormal operand/reciprocal/
+ * quotient) and no v_div_fixup special case. */
+__device__ __forceinline__ bool den_ok(float d)
+{
+    u32 b = __float_as_uint(d) & 0x7fffffffu;
+    return b - 0x30800000u <= 0x4e800000u - 0x30800000u;
+}
+__device__ __forceinline__ bool num_ok(float n)
+{
+    u32 b = __float_as_uint(n) & 0x7fffffffu;
+    return b - 0x21800000u <= 0x5d800000u - 0x21800000u;
+}
+__device__ __forceinline__ float div_core(float n, const Rcp &R)
+{
+    float q = n * R.r;
+    float e = __builtin_fmaf(-R.d, q, n);
+    q = __builtin_fmaf(e, R.r, q);
+    e = __builtin_fmaf(-R.d, q, n);
+    return __builtin_fmaf(e, R.r, q);
+}
+/* n / R.d, bitwise equal to the compiler's correctly rounded division;
+ * `dok` = den_ok(R.d), evaluated once per denominator. */
+__device__ __forceinline__ float cdiv(float n, const Rcp &R, bool dok)
+{
+    float q = div_core(n, R);
+    if (!(dok && num_ok(n)))
+        q = n / R.d;
+    return q;
+}
+__device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
+{
+    float m = csqrt(dot(v, v));
+    if (m == 0.0f)
+        m = 1.0f;
+    Rcp R = mkrcp(m);
+    bool dok = den_ok(m);
+    return mk(cdiv(v.x, R, dok), cdiv(v.y, R, dok), cdiv(v.z, R, dok));
+}
 /* (int)x as x86 cvttss2si: out-of-range and NaN give INT_MIN (the reference
  * runs on x86; v_cvt_i32_f32 would saturate / give 0). */
 __device__ __forceinline__ int cvt_x86(float x)
@@ -199,6 +275,41 @@ __device__ __forceinline__ float u11(u32 o)
     return r;
 }
 
+/* --------------------------------------------------------- wave helpers --- */
+__device__ __forceinline__ float rdlane(float v, int l)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+__device__ __forceinline__ V3 univ(V3 v) { return mk(unif(v.x), unif(v.y), unif(v.z)); }
+__device__ __forceinline__ int nth_set_bit(u64 m, int k) /* 1-based k, m has >= k bits */
+{
+    for (int j = 1; j < k; j++)
+        m &= m - 1;
+    return __builtin_ctzll(m);
+}
+/* 64-wide pairwise tree sum, identical in every lane: ((a0+a1)+(a2+a3))+...
+ * Levels 1-4 run in DPP (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+ * row_mirror): after level k every aligned group of 2^k lanes holds the same
+ * partial sum, so a mirror partner is as good as the xor partner and IEEE
+ * commutativity makes each lane's sum bitwise equal.  The four row sums are
+ * then combined as (r0 + r1) + (r2 + r3) through readlane -- no LDS traffic. */
+template <int CTRL>
+__device__ __forceinline__ float dpp_partner(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_tree_sum(float v)
+{
+    v = v + dpp_partner<0xB1>(v);  /* quad_perm [1,0,3,2]: lane ^ 1 */
+    v = v + dpp_partner<0x4E>(v);  /* quad_perm [2,3,0,1]: lane ^ 2 */
+    v = v + dpp_partner<0x141>(v); /* row_half_mirror: partner in the other quad of the 8 */
+    v = v + dpp_partner<0x140>(v); /* row_mirror: partner in the other 8 of the row */
+    float r0 = rdlane(v, 0), r1 = rdlane(v, 16), r2 = rdlane(v, 32), r3 = rdlane(v, 48);
+    return (r0 + r1) + (r2 + r3);
+}
+
 /* ----------------------------------------------------------- CSG spans --- */
 /* Compact span: a boundary is (t, ref); the reference's normal and material
  * (include/span.h:12-120) are functions of ref and recomputed only for the
@@ -235,22 +346,24 @@ struct Sph
     struct St
     {
         float t0, t1;
-        bool live;
+        int live; /* int, not bool: kept in a VGPR instead of an SGPR lane mask */
     };
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)
     {
-        c.omc = o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
-        c.c = dot(c.omc, c.omc) - e.P[OFF + 3];
+        c.omc = univ(o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+        c.c = unif(dot(c.omc, c.omc) - e.P[OFF + 3]);
     }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float a, const Env &)
     {
         float b = dot(c.omc, d);
         float disc = b * b - a * c.c;
-        s.live = !(disc <= EPS);
+        s.live = !(disc <= EPS) ? 1 : 0;
         if (s.live) {
-            float q = __builtin_sqrtf(disc);
-            s.t0 = (-b - q) / a;
-            s.t1 = (-b + q) / a;
+            float q = csqrt(disc);
+            Rcp R = mkrcp(a);
+            bool dok = den_ok(a);
+            s.t0 = cdiv(-b - q, R, dok);
+            s.t1 = cdiv(-b + q, R, dok);
         }
     }
     __device__ static __forceinline__ bool pull(St &s, CS &out)
@@ -259,7 +372,7 @@ struct Sph
             return false;
         out.t0 = s.t0, out.t1 = s.t1;
         out.r0 = mkref(PRIM, MAT, 0), out.r1 = mkref(PRIM, MAT, 1);
-        s.live = false;
+        s.live = 0;
         return true;
     }
     __device__ static __forceinline__ V3 normal(int, float t, V3 o, V3 d, const Env &e)
@@ -280,11 +393,11 @@ struct Pln
     struct St
     {
         float t0, t1;
-        bool live;
+        int live; /* int, not bool: kept in a VGPR instead of an SGPR lane mask */
     };
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)
     {
-        c.num = -e.P[OFF + 3] - dot(o, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+        c.num = unif(-e.P[OFF + 3] - dot(o, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2])));
     }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float, const Env &e)
     {
@@ -296,13 +409,13 @@ struct Pln
             deg = __builtin_fabsf(t) >= MAXV;
         }
         if (deg) {
-            s.live = __builtin_fabsf(c.num) < EPS * EPS;
+            s.live = __builtin_fabsf(c.num) < EPS * EPS ? 1 : 0;
             s.t0 = -MAXV, s.t1 = MAXV;
         } else if (div < 0.0f) {
-            s.live = true;
+            s.live = 1;
             s.t0 = t, s.t1 = MAXV;
         } else {
-            s.live = true;
+            s.live = 1;
             s.t0 = -MAXV, s.t1 = t;
         }
     }
@@ -312,7 +425,7 @@ struct Pln
             return false;
         out.t0 = s.t0, out.t1 = s.t1;
         out.r0 = mkref(PRIM, MAT, 0), out.r1 = mkref(PRIM, MAT, 1);
-        s.live = false;
+        s.live = 0;
         return true;
     }
     __device__ static __forceinline__ V3 normal(int, float, V3, V3, const Env &e)
@@ -336,7 +449,7 @@ struct Pln
         typename A::St a;                                                                           \
         typename B::St b;                                                                           \
         CS sa, sb;                                                                                  \
-        bool ea, eb;                                                                                \
+        int ea, eb; /* ints: VGPRs rather than SGPR lane masks */                                  \
     };                                                                                              \
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)                        \
     {                                                                                               \
@@ -492,7 +605,7 @@ struct Xf
         typename C::Ctx c;
     };
     typedef typename C::St St;
-    __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e) { C::prep(c.c, m_apply(e.P + MOFF, o), e); }
+    __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e) { C::prep(c.c, univ(m_apply(e.P + MOFF, o)), e); }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float, const Env &e)
     {
         V3 dl = m_lin(e.P + MOFF, d);
@@ -741,43 +854,22 @@ struct TSpherical
     __device__ static __forceinline__ float value(V3 p, const Env &e) { return T::value(spherical_map(p), e); }
 };
 
-/* --------------------------------------------------------- wave helpers --- */
-__device__ __forceinline__ float rdlane(float v, int l)
-{
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
-__device__ __forceinline__ V3 univ(V3 v) { return mk(unif(v.x), unif(v.y), unif(v.z)); }
-__device__ __forceinline__ int nth_set_bit(u64 m, int k) /* 1-based k, m has >= k bits */
-{
-    for (int j = 1; j < k; j++)
-        m &= m - 1;
-    return __builtin_ctzll(m);
-}
-/* 64-wide pairwise butterfly: lane i adds lane i^k for k = 1..32; IEEE
- * addition is commutative so every lane ends with the same tree sum. */
-__device__ __forceinline__ float wave_tree_sum(float v)
-{
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1)
-        v = v + __shfl_xor(v, k, 64);
-    return v;
-}
-
+/* Per-wave statistics, kept in LDS (every lane writes the same value). */
 struct Counters
 {
     u64 queries, leaf, attempts, rounds, shaded, nonleaf;
 };
 
 /* ---------------------------------------------------------------- spine --- */
-struct Frame /* one suspended traceRay activation (LDS) */
+/* One traceRay activation.  The current activation is F[sp]; all of its state
+ * lives in LDS and is read where it is used, so the hot burst loop carries no
+ * spine registers.  Every lane writes identical values. */
+struct Frame
 {
-    V3 d;
+    V3 o, d;
     float strength;
-    V3 hit;
     int depth;
-    V3 n;
+    V3 hit, n;
     int mat;
     V3 retval;
     float add;
@@ -785,36 +877,42 @@ struct Frame /* one suspended traceRay activation (LDS) */
     float rf;
     V3 rc;
     float sc;
-    V3 w;
-    int N;
-    int i;
-    int resume;
-    int pad0, pad1;
+    V3 w; /* weight of the child being traced */
+    int N, i, resume;
 };
 
 enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 
 /* Wave-cooperative scatter loop (path-trace.h:138-163) for sc > eps, from
- * child index i.  Returns B_DONE when all N children are summed, B_ABORT on the
- * reference's count > 1000 early return (path-trace.h:149-152), B_NONLEAF with
- * the next child's direction/factor when that child must recurse (it draws
- * random numbers, so it runs on the spine). */
+ * child index f.i.  Returns B_DONE when all N children are summed, B_ABORT on
+ * the reference's count > 1000 early return (path-trace.h:149-152), B_NONLEAF
+ * after writing the next child's ray into `child` when that child must
+ * recurse (it draws random numbers, so it runs on the spine). */
 template <class S, bool STRICT>
 __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
-                                     float4 *q, V3 hit, V3 n, V3 refl, V3 rc, float sc, float strength, float add,
-                                     int depth, int N, int &i, V3 &retval, V3 &nl_dir, float &nl_factor,
-                                     Counters &cnt)
+                                     float4 *q, Frame &f, Frame &child, Counters &cnt)
 {
-    const int lane = threadIdx.x;
-    const V3 kR = (1.0f / sc - 1.0f) * refl;          /* (1 / scatter_coefficient - 1) * reflectedRayDir */
-    const float sNa = (strength / (float)N) * add;    /* strength / scatter_ray_count * addFactor          */
-    const float aN = add / (float)N;                  /* addFactor / scatter_ray_count                      */
-    const float abs_rc = length(rc);
+    const int lane = threadIdx.x & 63;
+    const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
+    const float sc = unif(f.sc), strength = unif(f.strength), add = unif(f.add);
+    const int depth = uni(f.depth), N = uni(f.N);
+    int i = uni(f.i);
+    V3 retval = univ(f.retval);
+    const V3 kR = univ((1.0f / sc - 1.0f) * univ(f.refl)); /* (1 / scatter_coefficient - 1) * reflectedRayDir */
+    const float sNa = unif((strength / (float)N) * add);  /* strength / scatter_ray_count * addFactor           */
+    const float aN = unif(add / (float)N);                /* addFactor / scatter_ray_count                       */
+    const float abs_rc = unif(length(rc));
     const bool child_leaf_depth = depth - 1 <= 0;
-    typename S::Root::Ctx ctx;
-    S::Root::prep(ctx, hit, e);
+    /* Every child is provably a leaf when depth-1 <= 0 or when even the largest
+     * possible factor (1 + 4e-7: wn and n are unit vectors) keeps the child
+     * strength below eps.  Then acceptance needs no normalisation, and the
+     * normalised direction / factor are computed per child at trace time
+     * (same arithmetic, same bits) with every lane busy. */
+    const bool deferred = child_leaf_depth || (sNa * abs_rc * 1.01f < EPS);
     const u64 ginc = G3l * rng.inc;
+    const u64 A64 = jump[128], G64 = jump[129]; /* full round: 192 draws */
     int qhead = 0, qn = 0, fails = 0, reason = -1;
+    u64 n_rounds = 0, n_att = 0, n_leaf = 0;
     for (;;) {
         if (reason < 0 && qn < 64) {
             /* ---- generation round: lane l evaluates attempt l (draws 3l..3l+2) */
@@ -823,34 +921,37 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
             u64 s1 = s0 * PCG_MULT + rng.inc;
             u64 s2 = s1 * PCG_MULT + rng.inc;
             V3 v = mk(u11(pcg_out(s0)), u11(pcg_out(s1)), u11(pcg_out(s2)));
-            bool ball = !(length(v) > 1.0f);                 /* rand(): while (mag > max) */
+            /* rand(): while (mag > max) with mag = sqrt(|v|^2); correctly rounded
+             * sqrt(x) > 1  <=>  x > 1 + 2^-23 (exhaustively checked) */
+            bool ball = !(dot(v, v) > 0x1.000002p+0f);
             V3 w = v + kR;
             bool hemi = !(dot(n, w) <= EPS);                 /* while (dot(normal, dir) <= eps) */
             bool acc = ball && hemi;
-            V3 wn = mk(0, 0, 0);
+            V3 wn = w;
             float factor = 0.0f;
             bool leaf = true;
-            if (acc) {
-                wn = normalize(w);
+            if (!deferred && acc) {
+                wn = cnormalize(w);
                 factor = 1.0f - (1.0f - dot(wn, n)) * sc;
                 float cs = (sNa * factor) * abs_rc;
                 leaf = child_leaf_depth || cs < EPS;
             }
-            const u64 A = __ballot(acc), F = __ballot(ball && !hemi), NL = __ballot(acc && !leaf);
-            cnt.rounds++;
+            const u64 A = __ballot(acc), F = __ballot(ball && !hemi);
+            const u64 NL = deferred ? 0ull : __ballot(acc && !leaf);
+            n_rounds++;
             /* ---- replay the sequential consumption rule on the masks */
             const int nl = NL ? __builtin_ctzll(NL) : 64;
             const int pos_rem = (__popcll(A) >= (unsigned)rem) ? nth_set_bit(A, rem) : 64;
             int pos_abort = 64;
             if (fails + __popcll(F) >= 1000) {
-                int f = fails;
+                int fc = fails;
                 for (int l = 0; l < 64; l++) {
                     if (l == nl || l == pos_rem)
                         break;
                     if ((A >> l) & 1ull)
-                        f = 0;
+                        fc = 0;
                     else if ((F >> l) & 1ull) {
-                        if (++f == 1000) {
+                        if (++fc == 1000) {
                             pos_abort = l;
                             break;
                         }
@@ -865,8 +966,14 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
             } else if (nl < 64 && nl <= pos_rem) {
                 reason = B_NONLEAF, cut = nl;
                 take = A & ((1ull << cut) - 1ull);
-                nl_dir = mk(rdlane(wn.x, nl), rdlane(wn.y, nl), rdlane(wn.z, nl));
-                nl_factor = rdlane(factor, nl);
+                V3 nd = mk(rdlane(wn.x, nl), rdlane(wn.y, nl), rdlane(wn.z, nl));
+                float nf = rdlane(factor, nl);
+                /* w = addFactor / N * factor * reflect; strength = strength / N * addFactor * factor * |reflect| */
+                f.w = (aN * nf) * rc;
+                child.o = hit;
+                child.d = nd;
+                child.strength = (sNa * nf) * abs_rc;
+                child.depth = depth - 1;
             } else if (pos_rem < 64) {
                 reason = B_DONE, cut = pos_rem;
                 take = (cut == 63) ? A : (A & ((2ull << cut) - 1ull));
@@ -879,15 +986,19 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
                     fails += __popcll(F);
                 }
             }
-            cnt.attempts += (u64)(cut + 1);
+            n_att += (u64)(cut + 1);
             if ((take >> lane) & 1ull) {
                 int r = __popcll(take & ((1ull << lane) - 1ull));
                 q[(qhead + qn + r) & 127] = make_float4(wn.x, wn.y, wn.z, factor);
             }
             qn += __popcll(take);
             /* ---- advance the sample's stream past the consumed attempts */
-            const int m = cut + 1;
-            rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
+            if (cut == 63) {
+                rng.st = A64 * rng.st + G64 * rng.inc;
+            } else {
+                const int m = cut + 1;
+                rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
+            }
         }
         if (qn >= 64 || (reason >= 0 && qn > 0)) {
             /* ---- trace one batch of leaf children, one per lane */
@@ -896,6 +1007,12 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
             if (lane < cntb) {
                 float4 en = q[(qhead + lane) & 127];
                 V3 dir = mk(en.x, en.y, en.z);
+                if (deferred) {
+                    dir = cnormalize(dir);
+                    en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
+                }
+                typename S::Root::Ctx ctx;
+                S::Root::prep(ctx, hit, e);
                 float t;
                 u32 ref;
                 bool ex;
@@ -927,59 +1044,51 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
                 retval = retval + mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
                 retval = univ(retval);
             }
-            cnt.leaf += (u64)cntb;
+            n_leaf += (u64)cntb;
             qhead += cntb;
             qn -= cntb;
             i += cntb;
             continue;
         }
         if (reason >= 0)
-            return reason;
+            break;
     }
+    f.retval = retval;
+    f.i = i;
+    cnt.rounds += n_rounds;
+    cnt.attempts += n_att;
+    cnt.leaf += n_leaf;
+    return reason;
 }
 
 enum { PH_ENTER, PH_SETUP, PH_LOOP, PH_RETURN };
 enum { RS_REFRACT, RS_SCATTER };
 
 /* One sample = one traceRay tree (path-trace.h:58-165) + the jittered camera
- * ray of tracePixel (path-trace.h:190-198). */
+ * ray of tracePixel (path-trace.h:190-198).  F = this wave's frame stack. */
 template <class S, int MAXD, bool STRICT>
-__device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *stk, float4 *q,
+__device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, float4 *q,
                                            const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt)
 {
-    const int lane = threadIdx.x;
     Rng rng;
     rng_seed(rng, lp.seed, (u64)pix, (u64)s);
     const int px = pix % lp.W, py = pix / lp.W;
-    float x = 2.0f * ((float)px + u01(rng_next(rng))) / (float)lp.W - 1.0f;
-    float y = 1.0f - 2.0f * ((float)py + u01(rng_next(rng))) / (float)lp.H;
-    V3 o = mk(0, 0, 0), d = mk(x * lp.sw, y * lp.sh, -lp.dist);
-    float strength = 1.0f;
-    int depth = lp.depth;
+    {
+        float x = 2.0f * ((float)px + u01(rng_next(rng))) / (float)lp.W - 1.0f;
+        float y = 1.0f - 2.0f * ((float)py + u01(rng_next(rng))) / (float)lp.H;
+        F[0].o = mk(0, 0, 0);
+        F[0].d = mk(x * lp.sw, y * lp.sh, -lp.dist);
+        F[0].strength = 1.0f;
+        F[0].depth = lp.depth;
+    }
     int sp = 0;
-    V3 result = mk(0, 0, 0);
-    V3 hit = mk(0, 0, 0), n = mk(0, 0, 0), retval = mk(0, 0, 0), refl = mk(0, 0, 0), rc = mk(0, 0, 0),
-       w = mk(0, 0, 0);
-    int mat = 0, N = 1, i = 0, resume = 0;
-    float add = 1.0f, rf = 0.0f, sc = 0.0f;
     int phase = PH_ENTER;
-
-#define PTD_PUSH_AND_ENTER(RES, DIR, STRENGTH)                                                          \
-    do {                                                                                                \
-        if (lane == 0) {                                                                                \
-            Frame &f = stk[sp];                                                                         \
-            f.d = d, f.strength = strength, f.hit = hit, f.depth = depth, f.n = n, f.mat = mat;         \
-            f.retval = retval, f.add = add, f.refl = refl, f.rf = rf, f.rc = rc, f.sc = sc, f.w = w;    \
-            f.N = N, f.i = i, f.resume = (RES);                                                         \
-        }                                                                                               \
-        sp++;                                                                                           \
-        o = hit, d = (DIR), strength = (STRENGTH), depth = depth - 1;                                   \
-        phase = PH_ENTER;                                                                               \
-    } while (0)
-
+    V3 result = mk(0, 0, 0);
     for (;;) {
+        Frame &f = F[sp];
         if (phase == PH_ENTER) {
             cnt.queries++;
+            const V3 o = univ(f.o), d = univ(f.d);
             typename S::Root::Ctx ctx;
             S::Root::prep(ctx, o, e);
             float t = 0.0f;
@@ -990,12 +1099,15 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 phase = PH_RETURN;
                 continue;
             }
-            hit = o + t * d;
-            mat = ref_mat(ref);
+            t = unif(t);
+            ref = (u32)uni((int)ref);
+            const V3 hit = o + t * d;
+            const int mat = ref_mat(ref);
             V3 nn = S::Root::normal(ref_prim(ref), t, o, d, e);
             if (ref & FLIP)
                 nn = -nn;
             float ior;
+            V3 n;
             if (ex) {
                 n = -nn;
                 ior = S::ior(mat, e);
@@ -1003,126 +1115,158 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 n = nn;
                 ior = (float)(1.0 / (double)S::ior(mat, e));
             }
-            retval = S::emis(mat, hit, e);
-            add = 1.0f;
-            if (depth <= 0 || strength < EPS) {
+            const V3 retval = S::emis(mat, hit, e);
+            f.hit = hit, f.n = n, f.mat = mat, f.retval = retval, f.add = 1.0f;
+            const float strength = unif(f.strength);
+            if (uni(f.depth) <= 0 || strength < EPS) {
                 result = retval;
                 phase = PH_RETURN;
                 continue;
             }
             cnt.shaded++;
-            rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
+            const float rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
+            f.rf = rf;
             if (rf > EPS) {
                 V3 rd = refract(d, ior, n);
                 if (!is_zero(rd)) {
                     V3 tr = S::trans(mat, hit, e);
-                    w = (add * rf) * tr;
-                    float cs = strength * rf * add * length(tr);
-                    PTD_PUSH_AND_ENTER(RS_REFRACT, rd, cs);
+                    f.w = (1.0f * rf) * tr; /* addFactor * refractFactor * transmit, addFactor == 1 */
+                    f.resume = RS_REFRACT;
+                    Frame &c = F[sp + 1];
+                    c.o = hit, c.d = rd;
+                    c.strength = strength * rf * 1.0f * length(tr);
+                    c.depth = uni(f.depth) - 1;
+                    sp++;
                     continue;
                 }
             }
             phase = PH_SETUP;
         } else if (phase == PH_SETUP) {
+            const float add = unif(f.add);
             if (add < EPS) {
-                result = retval;
+                result = univ(f.retval);
                 phase = PH_RETURN;
                 continue;
             }
-            sc = clamp01(S::scat(mat, hit, e));
-            N = cvt_x86(10000.0f * strength * add * sc);
+            const int mat = uni(f.mat);
+            const V3 hit = univ(f.hit), n = univ(f.n);
+            const float sc = clamp01(S::scat(mat, hit, e));
+            int N = cvt_x86(10000.0f * unif(f.strength) * add * sc);
             if (sc <= EPS)
                 N = 1;
             if (N == 0)
                 N = 1;
-            rc = S::refl(mat, hit, e);
-            refl = reflect(d, n);
-            i = 0;
+            f.sc = sc, f.N = N, f.i = 0;
+            f.rc = S::refl(mat, hit, e);
+            f.refl = reflect(univ(f.d), n);
             phase = PH_LOOP;
         } else if (phase == PH_LOOP) {
-            if (i >= N) {
-                result = retval;
+            if (uni(f.i) >= uni(f.N)) {
+                result = univ(f.retval);
                 phase = PH_RETURN;
                 continue;
             }
-            if (sc > EPS) {
-                V3 nd;
-                float nf;
-                int why = burst<S, STRICT>(e, rng, jump, A3l, G3l, q, hit, n, refl, rc, sc, strength, add, depth, N,
-                                           i, retval, nd, nf, cnt);
+            if (unif(f.sc) > EPS) {
+                int why = burst<S, STRICT>(e, rng, jump, A3l, G3l, q, f, F[sp + 1], cnt);
                 if (why != B_NONLEAF) {
-                    result = retval;
+                    result = univ(f.retval);
                     phase = PH_RETURN;
                     continue;
                 }
                 cnt.nonleaf++;
-                w = ((add / (float)N) * nf) * rc;
-                float cs = (((strength / (float)N) * add) * nf) * length(rc);
-                PTD_PUSH_AND_ENTER(RS_SCATTER, nd, cs);
+                f.resume = RS_SCATTER;
+                sp++;
+                phase = PH_ENTER;
             } else {
+                const V3 refl = univ(f.refl), n = univ(f.n), rc = univ(f.rc);
+                const float sc = unif(f.sc), add = unif(f.add), N = (float)uni(f.N);
                 float factor = 1.0f - (1.0f - dot(refl, n)) * sc;
-                w = ((add / (float)N) * factor) * rc;
-                float cs = (((strength / (float)N) * add) * factor) * length(rc);
-                PTD_PUSH_AND_ENTER(RS_SCATTER, refl, cs);
+                f.w = ((add / N) * factor) * rc;
+                f.resume = RS_SCATTER;
+                Frame &c = F[sp + 1];
+                c.o = univ(f.hit), c.d = refl;
+                c.strength = (((unif(f.strength) / N) * add) * factor) * length(rc);
+                c.depth = uni(f.depth) - 1;
+                sp++;
+                phase = PH_ENTER;
             }
         } else { /* PH_RETURN */
             if (sp == 0)
                 break;
             sp--;
-            const Frame &f = stk[sp];
-            d = f.d, strength = f.strength, hit = f.hit, depth = f.depth, n = f.n, mat = f.mat;
-            V3 r0 = f.retval;
-            add = f.add, refl = f.refl, rf = f.rf, rc = f.rc, sc = f.sc, w = f.w, N = f.N, i = f.i;
-            resume = f.resume;
-            retval = r0 + w * result;
-            if (resume == RS_REFRACT) {
-                add *= 1.0f - rf;
+            Frame &p = F[sp];
+            p.retval = univ(p.retval) + univ(p.w) * result;
+            if (uni(p.resume) == RS_REFRACT) {
+                p.add = unif(p.add) * (1.0f - unif(p.rf));
                 phase = PH_SETUP;
             } else {
-                i += 1;
+                p.i = uni(p.i) + 1;
                 phase = PH_LOOP;
             }
         }
     }
-#undef PTD_PUSH_AND_ENTER
     /* tracePixel with one sample: (Color(0,0,0) + traceRay(...)) / 1 */
     V3 z = mk(0, 0, 0);
     return (z + result) / 1.0f;
 }
 
-/* The megakernel body: this wave traces items [64*chunk, 64*chunk + 64). */
+#ifndef PT_WPW
+#define PT_WPW 4 /* independent waves per workgroup */
+#endif
+#ifndef PT_CHUNK
+#define PT_CHUNK 16 /* (pixel, sample) items a wave takes per dequeue (<= 64) */
+#endif
+
+/* The megakernel body.  Persistent: the grid is sized to the resident
+ * capacity and every wave pulls 64-item chunks from a global counter until
+ * none are left.  Per-chunk cost varies by ~10^5 (sky pixels vs diffuse
+ * pixels), so static assignment or one-chunk-per-wave launches leave most
+ * SIMDs idle behind the slowest wave of each workgroup. */
 template <class S, int MAXD, bool STRICT>
 __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const PtImage *__restrict__ imgs,
                                              const u64 *__restrict__ jump, float *__restrict__ out,
                                              const int *__restrict__ pixels, u64 *__restrict__ stats,
                                              const PtLaunch &lp)
 {
-    __shared__ Frame stk[MAXD + 1];
-    __shared__ float4 q[128];
-    const int lane = threadIdx.x;
+    __shared__ Frame stk[PT_WPW][MAXD + 1];
+    __shared__ float4 qbuf[PT_WPW][128];
+    __shared__ Counters cbuf[PT_WPW];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const Env e = {P, imgs};
-    const long long item0 = (lp.chunk0 + (long long)blockIdx.x) * 64;
     const u64 A3l = jump[2 * lane], G3l = jump[2 * lane + 1];
-    Counters cnt = {0, 0, 0, 0, 0, 0};
-    V3 mine = mk(0, 0, 0);
-    for (int j = 0; j < 64; j++) {
-        const long long item = item0 + j;
-        if (item >= lp.n_items)
+    Counters &cnt = cbuf[wave];
+    cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = 0;
+    const long long n_chunks = (lp.n_items + PT_CHUNK - 1) / PT_CHUNK;
+    u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
+    for (;;) {
+        long long chunk = 0;
+        if (lane == 0)
+            chunk = (long long)atomicAdd(work, 1ull);
+        chunk = ((long long)uni((int)(chunk >> 32)) << 32) | (long long)(u32)uni((int)chunk);
+        if (chunk >= n_chunks)
             break;
-        const long long slot = item / lp.nsamp;
-        const int s = lp.s0 + (int)(item - slot * lp.nsamp);
-        const int pix = pixels ? pixels[slot] : (int)slot;
-        V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk, q, jump, A3l, G3l, cnt);
-        if (lane == j)
-            mine = c;
+        const long long item0 = chunk * PT_CHUNK;
+        V3 mine = mk(0, 0, 0);
+        for (int j = 0; j < PT_CHUNK; j++) {
+            const long long item = item0 + j;
+            if (item >= lp.n_items)
+                break;
+            const long long slot = item / lp.nsamp;
+            const int s = lp.s0 + (int)(item - slot * lp.nsamp);
+            const int pix = pixels ? pixels[slot] : (int)slot;
+            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], qbuf[wave], jump, A3l, G3l,
+                                                 cnt);
+            if (lane == j)
+                mine = c;
+        }
+        const long long my = item0 + lane;
+        if (lane < PT_CHUNK && my < lp.n_items) {
+            out[3 * my + 0] = mine.x;
+            out[3 * my + 1] = mine.y;
+            out[3 * my + 2] = mine.z;
+        }
     }
-    const long long my = item0 + lane;
-    if (my < lp.n_items) {
-        out[3 * my + 0] = mine.x;
-        out[3 * my + 1] = mine.y;
-        out[3 * my + 2] = mine.z;
-    }
-    if (lane == 0 && stats) {
+    if (lane == 0) {
         atomicAdd(&stats[0], cnt.queries);
         atomicAdd(&stats[1], cnt.leaf);
         atomicAdd(&stats[2], cnt.attempts);
@@ -1143,11 +1287,11 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         float *__restrict__ out, const int *__restrict__ pixels, u64 *__restrict__ stats, ptd::PtLaunch lp
 
 #define PT_DEFINE_KERNELS(SCENE, MAXD)                                                                      \
-    extern "C" __global__ __launch_bounds__(64, PT_MIN_WAVES) void pt_render_fast(PT_RENDER_ARGS)           \
+    extern "C" __global__ __launch_bounds__(64 * PT_WPW, PT_MIN_WAVES) void pt_render_fast(PT_RENDER_ARGS)  \
     {                                                                                                       \
         ptd::render_chunk<SCENE, MAXD, false>(P, imgs, jump, out, pixels, stats, lp);                      \
     }                                                                                                       \
-    extern "C" __global__ __launch_bounds__(64) void pt_render_strict(PT_RENDER_ARGS)                       \
+    extern "C" __global__ __launch_bounds__(64 * PT_WPW, PT_MIN_WAVES) void pt_render_strict(PT_RENDER_ARGS)\
     {                                                                                                       \
         ptd::render_chunk<SCENE, MAXD, true>(P, imgs, jump, out, pixels, stats, lp);                       \
     }
@@ -1189,5 +1333,50 @@ extern "C" __global__ __launch_bounds__(256) void pt_reduce(const float *__restr
         accum[3 * slot + 1] = ay;
         accum[3 * slot + 2] = az;
     }
+}
+#endif
+
+#ifdef PT_SELFTEST
+/* Bitwise check of the exact fast paths (csqrt, cdiv, cnormalize) against the
+ * compiler's correctly rounded sqrtf and '/', on n hashed inputs: half drawn
+ * from all 2^32 bit patterns, half with exponents around the fast ranges. */
+__device__ __forceinline__ float pt_st_float(u64 h, int mode)
+{
+    u32 b = (u32)h;
+    if (mode) {
+        u32 e = 40u + (u32)((h >> 32) % 180u); /* biased exponent 40..219 */
+        b = (b & 0x807fffffu) | (e << 23);
+    }
+    return __uint_as_float(b);
+}
+__device__ __forceinline__ bool pt_st_same(float a, float b)
+{
+    return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+}
+extern "C" __global__ void pt_selftest_math(u64 n, u64 seed, unsigned long long *bad)
+{
+    unsigned long long bs = 0, bd = 0, bn = 0;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        u64 h1 = ptd::splitmix64(seed ^ (i * 3)), h2 = ptd::splitmix64(seed ^ (i * 3 + 1)),
+            h3 = ptd::splitmix64(seed ^ (i * 3 + 2));
+        int mode = (int)(i & 1);
+        float x = pt_st_float(h1, mode), y = pt_st_float(h2, mode), z = pt_st_float(h3, mode);
+        if (!pt_st_same(ptd::csqrt(__builtin_fabsf(x)), __builtin_sqrtf(__builtin_fabsf(x))))
+            bs++;
+        ptd::Rcp R = ptd::mkrcp(y);
+        if (!pt_st_same(ptd::cdiv(x, R, ptd::den_ok(y)), x / y))
+            bd++;
+        float sc = mode ? 1.0f : 1e-30f;
+        ptd::V3 v = ptd::mk(x * sc, y * sc, z * sc);
+        ptd::V3 a = ptd::cnormalize(v), b = ptd::normalize(v);
+        if (!(pt_st_same(a.x, b.x) && pt_st_same(a.y, b.y) && pt_st_same(a.z, b.z)))
+            bn++;
+    }
+    if (bs)
+        atomicAdd(&bad[0], bs);
+    if (bd)
+        atomicAdd(&bad[1], bd);
+    if (bn)
+        atomicAdd(&bad[2], bn);
 }
 #endif

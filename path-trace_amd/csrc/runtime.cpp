@@ -95,6 +95,8 @@ struct DeviceState
     std::string key;
     hipModule_t mod = nullptr;
     hipFunction_t fast = nullptr, strict = nullptr, reduce = nullptr;
+    int wpw = 1; /* waves (chunks of 64 items) per workgroup, from the kernel's launch bounds */
+    int resident_blocks = 0; /* persistent grid size: resident workgroups per CU x CUs */
     std::vector<float> params;
     DevBuf<float> P;
     DevBuf<PtImageDev> imgs;
@@ -427,6 +429,15 @@ DeviceState &device_state(SceneImpl &s, int device, const Generated &g)
         HIPCHECK(hipModuleGetFunction(&ds->fast, ds->mod, "pt_render_fast"));
         HIPCHECK(hipModuleGetFunction(&ds->strict, ds->mod, "pt_render_strict"));
         HIPCHECK(hipModuleGetFunction(&ds->reduce, ds->mod, "pt_reduce"));
+        int mt = 0;
+        HIPCHECK(hipFuncGetAttribute(&mt, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, ds->fast));
+        if (mt < 64 || mt % 64)
+            throw Error(PT_ERR_DEVICE, "unexpected megakernel block size " + std::to_string(mt));
+        ds->wpw = mt / 64;
+        int per_cu = 0, cus = 0;
+        HIPCHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ds->fast, mt, 0));
+        HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        ds->resident_blocks = std::max(1, per_cu) * std::max(1, cus);
         ds->key = g.key;
     }
     if (ds->params != g.params) {
@@ -475,21 +486,8 @@ void validate(const pt_render_params *p)
     }
 }
 
-void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream_t stream, pt_render_stats *st)
+long long pass_samples(const pt_render_params *p, long long npix)
 {
-    validate(p);
-    Generated g = generate(s, p->depth);
-    s.last_key = g.key;
-    DeviceState &ds = device_state(s, p->device, g);
-    const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
-    if (npix == 0)
-        return;
-    const int *dpix = nullptr;
-    if (p->pixels) {
-        ds.pixels.ensure((size_t)npix);
-        HIPCHECK(hipMemcpyAsync(ds.pixels.p, p->pixels, (size_t)npix * 4, hipMemcpyHostToDevice, stream));
-        dpix = ds.pixels.p;
-    }
     int64_t budget = p->max_buffer_bytes > 0 ? p->max_buffer_bytes : (8ll << 30);
     long long per_pass = budget / (12ll * npix);
     per_pass = per_pass / 64 * 64;
@@ -497,13 +495,44 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
         per_pass = 64;
     if (per_pass > p->spp)
         per_pass = p->spp;
-    ds.stage.ensure((size_t)(npix * per_pass * 3));
-    if (p->spp > per_pass)
-        ds.accum.ensure((size_t)npix * 3);
-    if (st) {
-        memset(st, 0, sizeof(*st));
-        HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 16 * 8, stream));
+    return per_pass;
+}
+
+/* Module, parameters and every device buffer a render with p needs. */
+DeviceState &prepare(SceneImpl &s, const pt_render_params *p, Generated &g)
+{
+    validate(p);
+    g = generate(s, p->depth);
+    s.last_key = g.key;
+    DeviceState &ds = device_state(s, p->device, g);
+    const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
+    if (npix > 0) {
+        long long per_pass = pass_samples(p, npix);
+        ds.stage.ensure((size_t)(npix * per_pass * 3));
+        if (p->spp > per_pass)
+            ds.accum.ensure((size_t)npix * 3);
+        if (p->pixels)
+            ds.pixels.ensure((size_t)npix);
     }
+    return ds;
+}
+
+void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream_t stream, pt_render_stats *st)
+{
+    Generated g;
+    DeviceState &ds = prepare(s, p, g);
+    const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
+    if (npix == 0)
+        return;
+    const int *dpix = nullptr;
+    if (p->pixels) {
+        HIPCHECK(hipMemcpyAsync(ds.pixels.p, p->pixels, (size_t)npix * 4, hipMemcpyHostToDevice, stream));
+        dpix = ds.pixels.p;
+    }
+    const long long per_pass = pass_samples(p, npix);
+    if (st)
+        memset(st, 0, sizeof(*st));
+    HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 16 * 8, stream));
     hipFunction_t fn = p->order == PT_ORDER_REFERENCE ? ds.strict : ds.fast;
     std::vector<hipEvent_t> evs;
     auto event = [&]() {
@@ -517,10 +546,11 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
     for (int s0 = 0; s0 < p->spp; s0 += (int)per_pass) {
         int nsamp = (int)std::min<long long>(per_pass, p->spp - s0);
         long long n_items = npix * nsamp;
-        long long chunks = (n_items + 63) / 64;
-        const long long max_grid = 1ll << 30;
-        for (long long c0 = 0; c0 < chunks; c0 += max_grid) {
-            long long nc = std::min(max_grid, chunks - c0);
+        long long chunks = (n_items + 15) / 16;
+        const int wpw = ds.wpw;
+        {
+            long long blocks = std::min<long long>(ds.resident_blocks, (chunks + wpw - 1) / wpw);
+            long long c0 = 0;
             PtLaunchHost lp;
             memset(&lp, 0, sizeof lp);
             lp.seed = p->seed;
@@ -536,12 +566,14 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             const uint64_t *jp = ds.jump.p;
             float *op = ds.stage.p;
             const int *pp = dpix;
-            uint64_t *sp = st ? ds.stats.p : nullptr;
+            uint64_t *sp = ds.stats.p; /* counters + the persistent chunk counter (stats[15]) */
+            if (s0 > 0)
+                HIPCHECK(hipMemsetAsync(ds.stats.p + 15, 0, 8, stream));
             void *args[] = {&Pp, &ip, &jp, &op, &pp, &sp, &lp};
             int e0 = (int)evs.size();
             if (st)
                 event();
-            HIPCHECK(hipModuleLaunchKernel(fn, (unsigned)nc, 1, 1, 64, 1, 1, 0, stream, args, nullptr));
+            HIPCHECK(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 64 * wpw, 1, 1, 0, stream, args, nullptr));
             if (st) {
                 event();
                 spans.push_back({e0, e0 + 1});
@@ -876,6 +908,15 @@ const char *pt_scene_kernel_key(pt_scene *s, int depth)
     return k.c_str();
 }
 
+int pt_prepare(pt_scene *s, const pt_render_params *p)
+{
+    return guard([&] {
+        Generated g;
+        prepare(S(s), p, g);
+        return PT_OK;
+    });
+}
+
 int pt_render_device(pt_scene *s, const pt_render_params *p, float *fb, void *stream, pt_render_stats *stats)
 {
     return guard([&] {
@@ -914,6 +955,35 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
             for (int64_t k = 0; k < p->npixels; k++)
                 for (int c = 0; c < 3; c++) rgb_out[3 * k + c] = all[3 * (size_t)p->pixels[k] + c];
         }
+        return PT_OK;
+    });
+}
+
+/* Runs the device self-test of the exact sqrt/div fast paths on n inputs;
+ * mismatches[0..2] = sqrt, div, normalize mismatch counts (all 0 expected). */
+int pt_selftest_math(int device, uint64_t n, uint64_t seed, uint64_t *mismatches)
+{
+    return guard([&] {
+        if (!mismatches)
+            throw Error(PT_ERR_ARG, "null mismatches");
+        Generated g;
+        g.source = "#define PT_SELFTEST 1\n" + device_library_source();
+        g.key = "selftest";
+        const std::vector<char> &code = code_object(g);
+        HIPCHECK(hipSetDevice(device));
+        hipModule_t mod;
+        HIPCHECK(hipModuleLoadData(&mod, code.data()));
+        hipFunction_t fn;
+        HIPCHECK(hipModuleGetFunction(&fn, mod, "pt_selftest_math"));
+        uint64_t *bad = nullptr;
+        HIPCHECK(hipMalloc((void **)&bad, 32));
+        HIPCHECK(hipMemset(bad, 0, 32));
+        void *args[] = {&n, &seed, &bad};
+        HIPCHECK(hipModuleLaunchKernel(fn, 4096, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipMemcpy(mismatches, bad, 24, hipMemcpyDeviceToHost));
+        (void)hipFree(bad);
+        (void)hipModuleUnload(mod);
         return PT_OK;
     });
 }

@@ -26,7 +26,7 @@ from .scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTex
                     Sphere, Texture, TransformedObject, TransformedTexture, Union, invert, to_text,
                     transform_material, transform_object, transform_texture, union_array)
 
-__all__ = [n for n in dir() if not n.startswith("_")] + ["DeviceScene", "render", "render_device"]
+__all__ = [n for n in dir() if not n.startswith("_")] + ["DeviceScene", "render", "render_device", "prepare"]
 
 ORDERS = {"fast": PT_ORDER_GROUP64, "group64": PT_ORDER_GROUP64, "reference": PT_ORDER_REFERENCE,
           "strict": PT_ORDER_REFERENCE}
@@ -155,6 +155,11 @@ def render(scene, width: int, height: int, spp: int, depth: int, screen=None, se
     if keep is None:
         out = out.reshape(height, width, 3)
     return (out, st.as_dict()) if stats else out
+
+
+def prepare(scene: DeviceScene, params: RenderParams) -> None:
+    """Load/upload/allocate everything a render with `params` needs."""
+    _lib.check(_lib.lib().pt_prepare(scene.handle, ctypes.byref(params)))
 
 
 def render_device(scene: DeviceScene, params: RenderParams, fb_ptr: int, stream_ptr: int = 0, stats: bool = False):

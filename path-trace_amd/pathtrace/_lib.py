@@ -76,8 +76,10 @@ SIGNATURES = {
     "pt_matrix_concat": (None, [_FP, _FP, _FP]),
     "pt_render": (_I, [_P, ctypes.POINTER(RenderParams), _P, ctypes.POINTER(RenderStats)]),
     "pt_render_device": (_I, [_P, ctypes.POINTER(RenderParams), _P, _P, ctypes.POINTER(RenderStats)]),
+    "pt_prepare": (_I, [_P, ctypes.POINTER(RenderParams)]),
     "pt_scene_compile": (_I, [_P, _I]),
     "pt_scene_kernel_key": (ctypes.c_char_p, [_P, _I]),
+    "pt_selftest_math": (_I, [_I, ctypes.c_uint64, ctypes.c_uint64, _P]),
     "pt_write_hdr": (_I, [ctypes.c_char_p, _P, _I, _I]),
     "pt_write_bmp": (_I, [ctypes.c_char_p, _P, _I, _I, _I]),
 }
@@ -125,6 +127,12 @@ def matrix_concat(a, b):
     out = (ctypes.c_float * 12)()
     lib().pt_matrix_concat(_f12(a), _f12(b), out)
     return [np.float32(v) for v in out]
+
+
+def selftest_math(n: int = 1 << 26, seed: int = 1, device: int = 0):
+    out = np.zeros(3, dtype=np.uint64)
+    check(lib().pt_selftest_math(device, n, seed, out.ctypes.data))
+    return dict(zip(["sqrt", "div", "normalize"], [int(v) for v in out]))
 
 
 def load_hdr(path: str) -> np.ndarray:

@@ -36,3 +36,11 @@ def test_small_frame_bitexact(built, tmp_path, name, depth, order):
     assert diff[0].size == 0, "first mismatches: %s gpu=%s oracle=%s" % (
         diff[0][:5], g[diff[0][:5]], o[diff[0][:5]])
     assert np.all(rmse(g, o) <= RMSE_BAR)
+
+
+def test_fast_math_paths_bitexact(built):
+    """The megakernel's csqrt/cdiv/cnormalize are bit-identical to the
+    compiler's correctly rounded sqrtf and '/' (2^28 hashed inputs)."""
+    from pathtrace import _lib
+    bad = _lib.selftest_math(n=1 << 28, seed=12345)
+    assert bad == {"sqrt": 0, "div": 0, "normalize": 0}, bad
