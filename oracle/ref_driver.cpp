@@ -22,6 +22,7 @@
  *   kat     out.bin                          engine / math known-answer vectors
  *   hdr     in.hdr out_rgba.bin out_rewritten.hdr   reference HDR read + writeHDR
  *   writehdr w h rgba.bin out.hdr            reference MutableImage::writeHDR
+ *   matrix  in.bin out.bin                   Matrix::rotate / invert / concat
  */
 #include "path-trace.h"
 #include "image.h"
@@ -36,6 +37,7 @@
 #include <chrono>
 #include <cstdio>
 #include <fstream>
+#include <limits>
 #include <map>
 #include <thread>
 
@@ -390,6 +392,43 @@ int mode_writehdr(int argc, char **argv)
     return 0;
 }
 
+/* matrix: in.bin = n records of {float axis[3]; float pad; double angle; float m[12]; float m2[12]},
+ * out.bin = n records of {rotate(axis, angle)[12], invert(m)[12] (NaN if singular), m.concat(m2)[12]}. */
+int mode_matrix(int argc, char **argv)
+{
+    if (argc != 4)
+        return 2;
+    std::vector<char> raw = read_file(argv[2]);
+    const size_t rec = 4 * 4 + 8 + 48 + 48;
+    size_t n = raw.size() / rec;
+    std::vector<float> out;
+    auto put = [&](const Matrix &m) {
+        float v[12] = {m.x00, m.x10, m.x20, m.x30, m.x01, m.x11, m.x21, m.x31, m.x02, m.x12, m.x22, m.x32};
+        out.insert(out.end(), v, v + 12);
+    };
+    for (size_t k = 0; k < n; k++) {
+        const char *r = raw.data() + k * rec;
+        float axis[3];
+        double angle;
+        float m[12], m2[12];
+        memcpy(axis, r, 12);
+        memcpy(&angle, r + 16, 8);
+        memcpy(m, r + 24, 48);
+        memcpy(m2, r + 72, 48);
+        std::vector<float> mv(m, m + 12), m2v(m2, m2 + 12);
+        put(Matrix::rotate(Vector3D(axis[0], axis[1], axis[2]), angle));
+        try {
+            put(invert(mat12(mv, 0)));
+        } catch (std::domain_error &) {
+            float nan = std::numeric_limits<float>::quiet_NaN();
+            for (int j = 0; j < 12; j++) out.push_back(nan);
+        }
+        put(mat12(mv, 0).concat(mat12(m2v, 0)));
+    }
+    write_file(argv[3], out.data(), out.size() * 4);
+    return 0;
+}
+
 } // namespace
 
 int main(int argc, char **argv)
@@ -408,6 +447,8 @@ int main(int argc, char **argv)
             return mode_hdr(argc, argv);
         if (m == "writehdr")
             return mode_writehdr(argc, argv);
+        if (m == "matrix")
+            return mode_matrix(argc, argv);
         fprintf(stderr, "unknown mode %s\n", m.c_str());
         return 2;
     } catch (std::exception &e) {

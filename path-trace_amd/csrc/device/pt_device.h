@@ -802,7 +802,7 @@ __device__ __forceinline__ float log_filter(float v) /* filter_texture.h:66-71 *
 {
     if ((double)v <= 1e-30)
         return 0.0f;
-    return 0.5f + (float)__builtin_log((double)v) / 0.693147182f / 256.0f;
+    return 0.5f + (float)log((double)v) / 0.693147182f / 256.0f;
 }
 template <class T>
 struct TLog /* LogTexture */
@@ -833,12 +833,12 @@ __device__ __forceinline__ V3 spherical_map(V3 v) /* transform_texture.h:73-85 *
     if (is_zero(v))
         return mk(0, 0, 0);
     v = normalize(v);
-    float theta = (float)__builtin_atan2((double)v.y, (double)v.x);
+    float theta = (float)atan2((double)v.y, (double)v.x);
     if ((double)theta < -PI)
         theta = (float)((double)theta + 2 * PI);
     if ((double)theta > PI)
         theta = (float)((double)theta - 2 * PI);
-    float phi = (float)__builtin_asin((double)v.z);
+    float phi = (float)asin((double)v.z);
     return mk((float)((double)theta * 0.5 / PI + 0.5), (float)((double)phi / (PI / 2) * 0.5 + 0.5), 0);
 }
 template <class T>

@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
+#include <utime.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -109,8 +110,10 @@ const std::vector<char> &code_object(const Generated &g)
         std::ifstream f(path, std::ios::binary);
         if (f) {
             std::vector<char> code((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-            if (!code.empty())
+            if (!code.empty()) {
+                utime(path.c_str(), nullptr); /* mark as used (build() prunes unused objects) */
                 return g_mem[key] = std::move(code);
+            }
         }
     }
     std::string log;

@@ -1,6 +1,6 @@
 """Multi-GPU sharding of one frame.
 
-The frame is cut into 16x16 tiles; tile k belongs to rank hash(k) mod N
+The frame is cut into 16x16 tiles dealt round-robin to ranks in hashed order
 (interleaved: tile cost varies by ~10^3 between sky and diffuse regions, so
 contiguous bands would load-imbalance).  Every pixel has exactly one owner
 and its samples are seeded by its global index, so each rank writes its own
@@ -32,7 +32,11 @@ def rank_pixels(width: int, height: int, rank: int, world: int, tile: int = TILE
         return np.arange(width * height, dtype=np.int32)
     tx = (width + tile - 1) // tile
     ty = (height + tile - 1) // tile
-    owners = tile_owner(np.arange(tx * ty), world).reshape(ty, tx)
+    # deal tiles round-robin in hashed order: spatially scattered, counts equal to +-1
+    order = np.argsort(tile_owner(np.arange(tx * ty), 1 << 30), kind="stable")
+    owners = np.empty(tx * ty, dtype=np.int64)
+    owners[order] = np.arange(tx * ty) % world
+    owners = owners.reshape(ty, tx)
     ys, xs = np.mgrid[0:height, 0:width]
     mine = owners[ys // tile, xs // tile] == rank
     return (ys * width + xs)[mine].astype(np.int32)

@@ -1,0 +1,65 @@
+"""Multi-GPU sharding (pathtrace.dist) on CPU: the tile partition covers every
+pixel exactly once, and a world-size-2 gloo run (each rank renders its tiles,
+then one sum-reduce) reproduces the single-process frame bit for bit.  The
+per-rank renderer here is the CPU oracle (no GPU in this container); the
+reduce is the exact call bench.py makes over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from pathtrace import dist as ptdist
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_partition_is_exact_cover(world):
+    W, H = 100, 37
+    parts = [ptdist.rank_pixels(W, H, r, world) for r in range(world)]
+    allpix = np.concatenate(parts)
+    assert len(allpix) == W * H
+    assert len(np.unique(allpix)) == W * H
+    if world > 1:
+        sizes = [len(p) for p in parts]
+        assert min(sizes) > 0
+
+
+def test_partition_balance_1080p():
+    sizes = [len(ptdist.rank_pixels(1920, 1080, r, 8)) for r in range(8)]
+    assert max(sizes) / min(sizes) < 1.1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, txt, W, H, spp, depth, out_path):
+    import torch
+    import torch.distributed as dist
+    import oracle_py as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pix = ptdist.rank_pixels(W, H, rank, world, tile=4)
+    fb = torch.zeros(W * H * 3, dtype=torch.float32)
+    vals = O.render(txt, W, H, spp, depth, pixels=pix, threads=2, order=O.ORDER_GROUP64)
+    fb.view(-1, 3)[torch.from_numpy(pix.astype(np.int64))] = torch.from_numpy(vals)
+    ptdist.reduce_frame(fb)
+    if rank == 0:
+        np.save(out_path, fb.numpy())
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_bitexact(built, tmp_path):
+    import torch.multiprocessing as mp
+    import oracle_py as O
+    from pathtrace import scenes
+    from pathtrace.scene import to_text
+    W, H, spp, depth = 24, 16, 2, 8
+    txt = to_text(scenes.scene_p1(), str(tmp_path))
+    out = str(tmp_path / "fb.npy")
+    mp.spawn(_worker, args=(2, _free_port(), txt, W, H, spp, depth, out), nprocs=2, join=True)
+    got = np.load(out).reshape(-1, 3)
+    want = O.render(txt, W, H, spp, depth, order=O.ORDER_GROUP64)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -1,0 +1,99 @@
+"""Test scenes beyond the benchmark configs: every CSG operator, transformed
+objects, the Difference quirk, glossy/glass/mirror materials and every texture
+class of the reference (include/texture.h, image_texture.h, filter_texture.h,
+transform_texture.h).  Shared by tests/golden/make_golden.py (which freezes the
+reference's outputs) and the tests that compare against them."""
+import math
+
+import numpy as np
+
+from pathtrace.scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTexture,
+                             ImageSkyboxAlphaTexture, ImageSkyboxTexture, ImageTexture, Intersection, LogTexture,
+                             Material, Matrix, MirrorBallSkymapTexture, MultiplyTexture, Plane,
+                             SphericalCoordinatesSkymapTexture, Sphere, TransformedObject, TransformedTexture, Union,
+                             union_array)
+
+# explicit matrices (constructor order x00 x10 x20 x30 x01 x11 x21 x31 x02 x12 x22 x32)
+ROT_SCALE = Matrix(0.8, -0.36, 0.48, 0.3, 0.6, 0.48, -0.64, -0.2, 0.0, 0.8, 0.6, 0.5)
+SHEAR = Matrix(1.0, 0.25, 0.0, -0.1, 0.0, 1.5, 0.1, 0.05, 0.2, 0.0, 0.9, 0.0)
+
+
+def zoo_images(seed=3):
+    rng = np.random.default_rng(seed)
+    imgs = []
+    for (h, w) in [(23, 37), (16, 16), (16, 16), (16, 16), (16, 16), (16, 16), (16, 16)]:
+        a = rng.uniform(0, 2, size=(h, w, 4)).astype(np.float32)
+        a[..., 3] = rng.uniform(0, 1, size=(h, w)).astype(np.float32)
+        imgs.append(Image(a))
+    return imgs
+
+
+def csg_zoo():
+    diffuse = Material(ColorTexture(0.8, 0.7, 0.6), ColorTexture(1))
+    glossy = Material(ColorTexture(0.9), ColorTexture(0.3))
+    glass = Material(ColorTexture(0.7), ColorTexture(0), ColorTexture(0), ColorTexture(0.9, 0.95, 1.0), 1.45,
+                     ColorTexture(0.8))
+    mirror = Material(ColorTexture(0.99), ColorTexture(0))
+    emit = Material(ColorTexture(0), ColorTexture(0), ColorTexture(1.5, 1.2, 0.9))
+    sky = Material(ColorTexture(0), ColorTexture(0), ColorTexture(0.4, 0.6, 1.0))
+    lens = Intersection(Sphere((0.0, 0.2, -3.2), 0.9, glass), Sphere((0.0, 0.2, -4.6), 0.9, glass))
+    carved = Difference(Sphere((-1.1, -0.1, -4.0), 0.7, diffuse),
+                        Union(Sphere((-0.8, 0.2, -3.4), 0.45, glossy), Plane((0, 1, 0), (0, 0.3, 0), diffuse)))
+    # a hole inside, B covering A's end, B starting before A (the copyEndFromStart quirk)
+    quirk = Difference(Sphere((1.2, -0.2, -4.2), 0.6, mirror), Sphere((1.0, -0.2, -3.7), 0.4, glossy))
+    xf = TransformedObject(ROT_SCALE, Union(Sphere((0.4, -0.9, -4.5), 0.35, glossy),
+                                            Intersection(Plane((0, -1, 0), (0, -0.7, 0), diffuse),
+                                                         Sphere((0.4, -0.9, -4.5), 0.6, emit))))
+    nested = TransformedObject(SHEAR, TransformedObject(ROT_SCALE, Sphere((-0.3, 1.0, -5.0), 0.4, emit)))
+    floor = Plane((0, 1, 0), 1.0, diffuse)
+    return union_array([lens, carved, quirk, xf, nested, floor, Plane((0, 0, 1), 50, sky)])
+
+
+def texture_zoo(imgs=None):
+    imgs = imgs or zoo_images()
+    planar = imgs[0]
+    faces = imgs[1:7]
+    mb = Material(ColorTexture(0), ColorTexture(0),
+                  MultiplyTexture((0.5, 0.7, 0.9), MirrorBallSkymapTexture(ImageTexture(planar))))
+    sph = Material(ColorTexture(0), ColorTexture(0), SphericalCoordinatesSkymapTexture(ImageTexture(planar)))
+    box = Material(ColorTexture(0), ColorTexture(0), ImageSkyboxTexture(*faces))
+    alpha_sc = Material(TransformedTexture(SHEAR, ImageTexture(planar)), ImageAlphaTexture(planar))
+    box_alpha = Material(ColorTexture(0.6), ImageSkyboxAlphaTexture(*faces), LogTexture(ImageTexture(planar)))
+    coord = Material(ColorTexture(0), ColorTexture(0),
+                     MultiplyTexture((0.05, 0.05, 0.05),
+                                     TransformedTexture(ROT_SCALE, SphericalCoordinatesSkymapTexture(CoordTexture()))))
+    return union_array([
+        Sphere((-0.9, 0.0, -3.5), 0.5, alpha_sc),
+        Sphere((0.9, 0.0, -3.5), 0.5, box_alpha),
+        Sphere((0.0, 0.8, -4.5), 0.45, coord),
+        Sphere((0.0, -0.6, -3.2), 0.3, box),
+        Plane((0, 0, 1), 30, mb),
+        Plane((0, 1, 0), 1.2, sph),
+        Plane((0, -1, 0), 8, box),
+    ])
+
+
+def random_rays(n, seed=9, spread=1.0):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(-spread, spread, size=(n, 3)).astype(np.float32) * np.float32(0.5)
+    o[:, 2] += np.float32(-1.0)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d[:, 2] = -np.abs(d[:, 2]) - np.float32(0.2)
+    d *= rng.uniform(0.5, 3000, size=(n, 1)).astype(np.float32)
+    return np.concatenate([o, d], axis=1).astype(np.float32)
+
+
+# (name, builder, W, H, spp, depth) of the per-sample render goldens
+RENDER_CASES = [
+    ("p0", "scene_p0", 32, 24, 3, 4),
+    ("p1", "scene_p1", 32, 24, 3, 8),
+    ("csg", "csg_zoo", 32, 24, 3, 6),
+    ("tex", "texture_zoo", 32, 24, 3, 5),
+]
+
+
+def build(name):
+    from pathtrace import scenes
+    if hasattr(scenes, name):
+        return getattr(scenes, name)()
+    return globals()[name]()
