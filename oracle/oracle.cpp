@@ -394,7 +394,11 @@ struct MirrorBallTex : Tex /* transform_texture.h:33-59 */
     float value(V3 p) const override { return t->value(map(p)); }
 };
 
-struct SphericalTex : Tex /* transform_texture.h:61-85: atan2f, ::asin(double) */
+/* transform_texture.h:61-85.  atan2f; and `asin(v.z)` on a float is asinf:
+ * src/test.cpp:22 includes image_texture.h -> image.h:28 (`using namespace std;`
+ * at global scope) before transform_texture.h, so std::asin(float) wins
+ * overload resolution in the reference's translation unit. */
+struct SphericalTex : Tex
 {
     std::unique_ptr<Tex> t;
     static V3 map(V3 v)
@@ -407,7 +411,7 @@ struct SphericalTex : Tex /* transform_texture.h:61-85: atan2f, ::asin(double) *
             theta = (float)(theta + 2 * M_PI);
         if (theta > M_PI)
             theta = (float)(theta - 2 * M_PI);
-        float phi = (float)::asin((double)v.z);
+        float phi = std::asin(v.z);
         return V3((float)(theta * 0.5 / M_PI + 0.5), (float)(phi / (M_PI / 2) * 0.5 + 0.5), 0);
     }
     V3 color(V3 p) const override { return t->color(map(p)); }

@@ -4,6 +4,13 @@
  * next to libpt.so, overridable with PT_JIT_CACHE).  build() pre-populates the
  * cache for the benchmark scenes so the GPU box only loads code objects; an
  * unseen scene is compiled on first use (no GPU needed to compile).
+ *
+ * hiprtc is dlopen'ed by absolute path ($ROCM_PATH or /opt/rocm) rather than
+ * linked: a PyTorch process already holds torch's own libhiprtc.so (soname
+ * libhiprtc.so.7, an older compiler), which a plain NEEDED entry would bind
+ * to whenever torch is imported first -- the code objects would then depend
+ * on import order.  The HIP runtime itself (libamdhip64.so.7) is deliberately
+ * the process's one, so device pointers and streams from torch are valid here.
  */
 #include <dlfcn.h>
 #include <hip/hiprtc.h>
@@ -24,6 +31,46 @@ namespace pt
 
 namespace
 {
+
+struct Rtc
+{
+    decltype(&hiprtcCreateProgram) create;
+    decltype(&hiprtcCompileProgram) compile;
+    decltype(&hiprtcGetProgramLogSize) log_size;
+    decltype(&hiprtcGetProgramLog) log;
+    decltype(&hiprtcGetCodeSize) code_size;
+    decltype(&hiprtcGetCode) code;
+    decltype(&hiprtcDestroyProgram) destroy;
+    decltype(&hiprtcVersion) version;
+};
+
+const Rtc &rtc()
+{
+    static Rtc r = [] {
+        std::string root = getenv("ROCM_PATH") && *getenv("ROCM_PATH") ? getenv("ROCM_PATH") : "/opt/rocm";
+        std::string path = root + "/lib/libhiprtc.so.7";
+        void *h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!h)
+            throw Error(PT_ERR_COMPILE, "cannot load " + path + ": " + dlerror());
+        Rtc t;
+        auto sym = [&](const char *n) {
+            void *p = dlsym(h, n);
+            if (!p)
+                throw Error(PT_ERR_COMPILE, std::string("hiprtc symbol missing: ") + n);
+            return p;
+        };
+        t.create = (decltype(t.create))sym("hiprtcCreateProgram");
+        t.compile = (decltype(t.compile))sym("hiprtcCompileProgram");
+        t.log_size = (decltype(t.log_size))sym("hiprtcGetProgramLogSize");
+        t.log = (decltype(t.log))sym("hiprtcGetProgramLog");
+        t.code_size = (decltype(t.code_size))sym("hiprtcGetCodeSize");
+        t.code = (decltype(t.code))sym("hiprtcGetCode");
+        t.destroy = (decltype(t.destroy))sym("hiprtcDestroyProgram");
+        t.version = (decltype(t.version))sym("hiprtcVersion");
+        return t;
+    }();
+    return r;
+}
 
 const char *kOptions[] = {
     "--offload-arch=gfx950",
@@ -53,7 +100,7 @@ std::string cache_dir()
 std::string full_key(const Generated &g)
 {
     int maj = 0, min = 0;
-    hiprtcVersion(&maj, &min);
+    rtc().version(&maj, &min);
     std::ostringstream k;
     k << g.source << "\n";
     for (const char *o : kOptions) k << o << "\n";
@@ -73,25 +120,26 @@ std::map<std::string, std::vector<char>> g_mem;
 
 std::vector<char> compile(const Generated &g, std::string &log)
 {
+    const Rtc &R = rtc();
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, g.source.c_str(), "pt_scene.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    if (R.create(&prog, g.source.c_str(), "pt_scene.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         throw Error(PT_ERR_COMPILE, "hiprtcCreateProgram failed");
     int n = (int)(sizeof(kOptions) / sizeof(kOptions[0]));
-    hiprtcResult r = hiprtcCompileProgram(prog, n, kOptions);
+    hiprtcResult r = R.compile(prog, n, kOptions);
     size_t ls = 0;
-    hiprtcGetProgramLogSize(prog, &ls);
+    R.log_size(prog, &ls);
     log.assign(ls, '\0');
     if (ls)
-        hiprtcGetProgramLog(prog, &log[0]);
+        R.log(prog, &log[0]);
     if (r != HIPRTC_SUCCESS) {
-        hiprtcDestroyProgram(&prog);
+        R.destroy(&prog);
         throw Error(PT_ERR_COMPILE, "hiprtc compile failed: " + log.substr(0, 4000));
     }
     size_t cs = 0;
-    hiprtcGetCodeSize(prog, &cs);
+    R.code_size(prog, &cs);
     std::vector<char> code(cs);
-    hiprtcGetCode(prog, code.data());
-    hiprtcDestroyProgram(&prog);
+    R.code(prog, code.data());
+    R.destroy(&prog);
     return code;
 }
 

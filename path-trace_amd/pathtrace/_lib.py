@@ -92,6 +92,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise PtError("libpt.so not built: run `python path-trace_amd/build_ext.py` (%s)" % LIB_PATH)
+        # libpt binds the process's HIP runtime (soname libamdhip64.so.7).  torch
+        # loads its own copy under another file name; loading torch first makes
+        # libpt share it, so torch's device pointers/streams are valid in libpt
+        # and the process holds one runtime, not two competing for the device.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
