@@ -1,0 +1,729 @@
+/*
+ * PathTrace.hpp -- C++ host facade over the C ABI (pt.h) that mirrors the
+ * reference's scene API (namespace PathTrace of programmerjake/path-trace),
+ * so reference scene-building code compiles against it unchanged:
+ *
+ *   Vector3D / Color                 include/vector3d.h:36-162, include/color.h
+ *   Matrix                           include/transform.h:16-421 (float arithmetic via pt_matrix_*)
+ *   Image, MutableImage              include/image.h:48-212 (HDR load / writeHDR)
+ *   Texture + 11 subclasses          include/texture.h, image_texture.h, filter_texture.h,
+ *                                    transform_texture.h
+ *   Material                         include/material.h:10-43
+ *   Object, Sphere, Plane, Union,
+ *   Intersection, Difference,
+ *   TransformedObject, transform()   include/object.h, sphere.h, plane.h, union.h, ...
+ *   unionArray                       src/test.cpp:52-64
+ *
+ * What differs is the last step: instead of world->makeSpanIterator() and a
+ * per-pixel tracePixel<T> loop (include/path-trace.h:187-201, src/test.cpp:
+ * 441-465), a `Renderer` flattens the object graph through the C ABI once and
+ * renders whole frames / pixel lists on the GPU.  Each class carries the
+ * `flatten` hook SURVEY.md s8(b) calls for.  Ownership follows the reference:
+ * composites own their children, materials own their textures, objects do
+ * not own materials.  Errors surface as the reference's exception types
+ * (std::domain_error for a singular matrix, ImageLoadError / ImageStoreError)
+ * or PathTrace::DeviceError for device / compile failures.
+ *
+ * Header-only, C++11.  Link with libpt.so.
+ */
+#ifndef PT_PATHTRACE_HPP
+#define PT_PATHTRACE_HPP
+
+#include <cmath>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pt.h"
+
+namespace PathTrace
+{
+
+/* ---------------------------------------------------------------- errors -- */
+class ImageLoadError : public std::runtime_error
+{
+public:
+    explicit ImageLoadError(const std::string &msg) : std::runtime_error(msg) {}
+};
+class ImageStoreError : public std::runtime_error
+{
+public:
+    explicit ImageStoreError(const std::string &msg) : std::runtime_error(msg) {}
+};
+class DeviceError : public std::runtime_error
+{
+public:
+    int code;
+    DeviceError(int code, const std::string &msg) : std::runtime_error(msg), code(code) {}
+};
+
+inline int ptCheck(int rc)
+{
+    if (rc >= 0)
+        return rc;
+    std::string msg = pt_last_error();
+    if (rc == PT_ERR_MATH)
+        throw std::domain_error(msg);
+    if (rc == PT_ERR_IO)
+        throw ImageLoadError(msg);
+    throw DeviceError(rc, msg);
+}
+
+/* -------------------------------------------------------------- Vector3D -- */
+class Vector3D
+{
+public:
+    float x, y, z;
+    Vector3D() : x(0), y(0), z(0) {}
+    Vector3D(float x, float y, float z) : x(x), y(y), z(z) {}
+    Vector3D(float v) : x(v), y(v), z(v) {}
+    friend Vector3D operator+(const Vector3D &l, const Vector3D &r) { return Vector3D(l.x + r.x, l.y + r.y, l.z + r.z); }
+    friend Vector3D operator-(const Vector3D &l, const Vector3D &r) { return Vector3D(l.x - r.x, l.y - r.y, l.z - r.z); }
+    friend Vector3D operator*(const Vector3D &l, const Vector3D &r) { return Vector3D(l.x * r.x, l.y * r.y, l.z * r.z); }
+    friend Vector3D operator/(const Vector3D &l, const Vector3D &r) { return Vector3D(l.x / r.x, l.y / r.y, l.z / r.z); }
+    friend Vector3D operator/(const Vector3D &l, float r) { return Vector3D(l.x / r, l.y / r, l.z / r); }
+    friend Vector3D operator*(const Vector3D &l, float r) { return Vector3D(l.x * r, l.y * r, l.z * r); }
+    friend Vector3D operator*(float l, const Vector3D &r) { return r * l; }
+    Vector3D operator-() const { return Vector3D(-x, -y, -z); }
+    friend bool operator==(const Vector3D &l, const Vector3D &r) { return l.x == r.x && l.y == r.y && l.z == r.z; }
+    friend bool operator!=(const Vector3D &l, const Vector3D &r) { return !(l == r); }
+    Vector3D &operator+=(const Vector3D &r) { return *this = *this + r; }
+    Vector3D &operator-=(const Vector3D &r) { return *this = *this - r; }
+    Vector3D &operator*=(const Vector3D &r) { return *this = *this * r; }
+    Vector3D &operator/=(const Vector3D &r) { return *this = *this / r; }
+    Vector3D &operator*=(float r) { return *this = *this * r; }
+    Vector3D &operator/=(float r) { return *this = *this / r; }
+};
+
+/* same evaluation order as include/vector3d.h:121-141 */
+inline float dot(const Vector3D &l, const Vector3D &r)
+{
+    Vector3D v = l * r;
+    return v.x + v.y + v.z;
+}
+inline float abs_squared(const Vector3D &v) { return dot(v, v); }
+inline float abs(const Vector3D &v) { return std::sqrt(abs_squared(v)); }
+inline Vector3D normalize(const Vector3D &v)
+{
+    float m = abs(v);
+    return v / (m == 0 ? 1.0f : m);
+}
+inline Vector3D cross(const Vector3D &a, const Vector3D &b)
+{
+    return Vector3D(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+typedef Vector3D Color;
+
+/* ---------------------------------------------------------------- Matrix -- */
+class Matrix
+{
+public:
+    /* constructor order of include/transform.h:148-174 */
+    float x00, x10, x20, x30, x01, x11, x21, x31, x02, x12, x22, x32;
+    Matrix() : x00(1), x10(0), x20(0), x30(0), x01(0), x11(1), x21(0), x31(0), x02(0), x12(0), x22(1), x32(0) {}
+    Matrix(float x00, float x10, float x20, float x30, float x01, float x11, float x21, float x31, float x02,
+           float x12, float x22, float x32)
+        : x00(x00), x10(x10), x20(x20), x30(x30), x01(x01), x11(x11), x21(x21), x31(x31), x02(x02), x12(x12),
+          x22(x22), x32(x32)
+    {
+    }
+    explicit Matrix(const float m[12])
+        : Matrix(m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7], m[8], m[9], m[10], m[11])
+    {
+    }
+    void get(float m[12]) const
+    {
+        const float v[12] = {x00, x10, x20, x30, x01, x11, x21, x31, x02, x12, x22, x32};
+        for (int i = 0; i < 12; i++) m[i] = v[i];
+    }
+    static Matrix identity() { return Matrix(); }
+    static Matrix rotate(const Vector3D axis, const double angle)
+    {
+        const float a[3] = {axis.x, axis.y, axis.z};
+        float m[12];
+        pt_matrix_rotate(a, angle, m);
+        return Matrix(m);
+    }
+    static Matrix rotateX(double angle) { return rotate(Vector3D(1, 0, 0), angle); }
+    static Matrix rotateY(double angle) { return rotate(Vector3D(0, 1, 0), angle); }
+    static Matrix rotateZ(double angle) { return rotate(Vector3D(0, 0, 1), angle); }
+    static Matrix translate(Vector3D p) { return translate(p.x, p.y, p.z); }
+    static Matrix translate(float x, float y, float z) { return Matrix(1, 0, 0, x, 0, 1, 0, y, 0, 0, 1, z); }
+    static Matrix scale(float x, float y, float z) { return Matrix(x, 0, 0, 0, 0, y, 0, 0, 0, 0, z, 0); }
+    static Matrix scale(Vector3D s) { return scale(s.x, s.y, s.z); }
+    static Matrix scale(float s) { return scale(s, s, s); }
+    friend Matrix invert(const Matrix &m)
+    {
+        float a[12], o[12];
+        m.get(a);
+        ptCheck(pt_matrix_inverse(a, o)); /* std::domain_error if singular, transform.h:353-354 */
+        return Matrix(o);
+    }
+    Matrix concat(Matrix rt) const
+    {
+        float a[12], b[12], o[12];
+        get(a);
+        rt.get(b);
+        pt_matrix_concat(a, b, o);
+        return Matrix(o);
+    }
+    Vector3D apply(Vector3D v) const
+    {
+        return Vector3D(v.x * x00 + v.y * x10 + v.z * x20 + x30, v.x * x01 + v.y * x11 + v.z * x21 + x31,
+                        v.x * x02 + v.y * x12 + v.z * x22 + x32);
+    }
+};
+
+/* ---------------------------------------------------------------- images -- */
+/* Refcounted, immutable RGBA f32 image, row 0 on top (include/image.h:48-101). */
+class Image
+{
+public:
+    Image() {}
+    explicit Image(std::string fileName, std::string format = "")
+    {
+        (void)format; /* only Radiance HDR is decoded (PNG needs libpng) */
+        int w = 0, h = 0;
+        if (pt_hdr_read(fileName.c_str(), nullptr, &w, &h) != PT_OK)
+            throw ImageLoadError(pt_last_error());
+        std::shared_ptr<std::vector<float>> px(new std::vector<float>((size_t)w * h * 4));
+        if (pt_hdr_read(fileName.c_str(), px->data(), &w, &h) != PT_OK)
+            throw ImageLoadError(pt_last_error());
+        data_ = px, w_ = (unsigned)w, h_ = (unsigned)h;
+    }
+    Image(std::vector<float> rgba, unsigned w, unsigned h)
+        : data_(new std::vector<float>(std::move(rgba))), w_(w), h_(h)
+    {
+        if (data_->size() != (size_t)w * h * 4)
+            throw std::invalid_argument("Image: rgba size != w*h*4");
+    }
+    unsigned width() const { return w_; }
+    unsigned height() const { return h_; }
+    explicit operator bool() const { return data_ != nullptr; }
+    bool operator!() const { return data_ == nullptr; }
+    friend bool operator==(const Image &l, const Image &r) { return l.data_ == r.data_; }
+    friend bool operator!=(const Image &l, const Image &r) { return l.data_ != r.data_; }
+    Color getPixel(int x, int y) const /* src/image.cpp:366-380 */
+    {
+        if (!data_ || x < 0 || y < 0 || (unsigned)x >= w_ || (unsigned)y >= h_)
+            return Color(0);
+        const float *p = data_->data() + ((size_t)y * w_ + x) * 4;
+        return Color(p[0], p[1], p[2]);
+    }
+    float getPixelAlpha(int x, int y) const
+    {
+        if (!data_ || x < 0 || y < 0 || (unsigned)x >= w_ || (unsigned)y >= h_)
+            return 0;
+        return (*data_)[((size_t)y * w_ + x) * 4 + 3];
+    }
+    const float *rgba() const { return data_ ? data_->data() : nullptr; }
+
+private:
+    std::shared_ptr<const std::vector<float>> data_;
+    unsigned w_ = 0, h_ = 0;
+};
+
+class MutableImage /* include/image.h:103-212 */
+{
+public:
+    MutableImage(unsigned w, unsigned h) : data_((size_t)w * h * 4, 0.0f), w_(w), h_(h) {}
+    explicit MutableImage(const Image &img) : w_(img.width()), h_(img.height())
+    {
+        if (!img)
+            throw std::runtime_error("can't create MutableImage from empty Image");
+        data_.assign(img.rgba(), img.rgba() + (size_t)w_ * h_ * 4);
+    }
+    unsigned width() const { return w_; }
+    unsigned height() const { return h_; }
+    void setPixel(int x, int y, Color c)
+    {
+        if (x < 0 || y < 0 || (unsigned)x >= w_ || (unsigned)y >= h_)
+            return;
+        float *p = &data_[((size_t)y * w_ + x) * 4];
+        p[0] = c.x, p[1] = c.y, p[2] = c.z;
+    }
+    Color getPixel(int x, int y) const
+    {
+        if (x < 0 || y < 0 || (unsigned)x >= w_ || (unsigned)y >= h_)
+            return Color(0);
+        const float *p = &data_[((size_t)y * w_ + x) * 4];
+        return Color(p[0], p[1], p[2]);
+    }
+    void writeHDR(std::string fileName) const /* src/image.cpp:398-481 */
+    {
+        std::vector<float> rgb((size_t)w_ * h_ * 3);
+        for (size_t i = 0; i < (size_t)w_ * h_; i++)
+            for (int c = 0; c < 3; c++) rgb[3 * i + c] = data_[4 * i + c];
+        if (pt_write_hdr(fileName.c_str(), rgb.data(), (int)w_, (int)h_) != PT_OK)
+            throw ImageStoreError(pt_last_error());
+    }
+    operator Image() const { return Image(data_, w_, h_); }
+
+private:
+    std::vector<float> data_;
+    unsigned w_, h_;
+};
+
+/* ------------------------------------------------------------- flattening -- */
+class Texture;
+struct Material;
+class Object;
+
+/* Builds one pt_scene from a reference-style object graph.  Shared materials,
+ * textures and images are flattened once. */
+class Flattener
+{
+public:
+    explicit Flattener(pt_scene *s) : s(s) {}
+    pt_scene *const s;
+    inline pt_id texture(const Texture *t);
+    inline pt_id material(const Material *m);
+    pt_id image(const Image &im)
+    {
+        if (!im)
+            throw std::invalid_argument("empty Image in a texture");
+        auto it = images_.find(im.rgba());
+        if (it != images_.end())
+            return it->second;
+        return images_[im.rgba()] = ptCheck(pt_image_from_rgba32f(s, im.rgba(), (int)im.width(), (int)im.height()));
+    }
+
+private:
+    std::map<const void *, pt_id> textures_, materials_, images_;
+};
+
+/* --------------------------------------------------------------- textures -- */
+class Texture /* include/texture.h:10-27 */
+{
+public:
+    virtual ~Texture() {}
+    virtual Texture *duplicate() const = 0;
+    virtual Texture *transform(const Matrix &) const { return nullptr; }
+    virtual pt_id flatten(Flattener &f) const = 0;
+};
+
+class ColorTexture : public Texture /* texture.h:29-58 */
+{
+public:
+    Color color;
+    ColorTexture(Color color) : color(color) {}
+    ColorTexture(float r, float g, float b) : color(r, g, b) {}
+    ColorTexture(float v) : color(v) {}
+    Texture *duplicate() const override { return new ColorTexture(color); }
+    Texture *transform(const Matrix &) const override { return new ColorTexture(color); }
+    pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_color(f.s, color.x, color.y, color.z)); }
+};
+
+class TransformedTexture : public Texture /* texture.h:60-90 */
+{
+public:
+    TransformedTexture(const Matrix &m, Texture *t) : m(m), t(t) {}
+    ~TransformedTexture() override { delete t; }
+    Texture *duplicate() const override { return new TransformedTexture(m, t->duplicate()); }
+    Texture *transform(const Matrix &m2) const override { return new TransformedTexture(m.concat(m2), t->duplicate()); }
+    pt_id flatten(Flattener &f) const override
+    {
+        float a[12];
+        m.get(a);
+        return ptCheck(pt_tex_transformed(f.s, a, f.texture(t)));
+    }
+
+private:
+    Matrix m;
+    Texture *t;
+};
+
+inline Texture *transform(const Matrix &m, Texture *t) /* texture.h:92-98 */
+{
+    Texture *r = t->transform(m);
+    return r ? r : new TransformedTexture(m, t->duplicate());
+}
+
+class ImageTexture : public Texture /* image_texture.h:9-33 */
+{
+public:
+    explicit ImageTexture(Image image) : image(image) {}
+    Texture *duplicate() const override { return new ImageTexture(image); }
+    pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_image(f.s, f.image(image))); }
+    Image image;
+};
+
+class ImageAlphaTexture : public Texture /* image_texture.h:35-70 */
+{
+public:
+    explicit ImageAlphaTexture(Image image) : image(image) {}
+    Texture *duplicate() const override { return new ImageAlphaTexture(image); }
+    pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_image_alpha(f.s, f.image(image))); }
+    Image image;
+};
+
+class ImageSkyboxTexture : public Texture /* image_texture.h:72-115 */
+{
+public:
+    ImageSkyboxTexture(Image top, Image bottom, Image left, Image right, Image front, Image back)
+        : faces{top, bottom, left, right, front, back}
+    {
+    }
+    Texture *duplicate() const override
+    {
+        return new ImageSkyboxTexture(faces[0], faces[1], faces[2], faces[3], faces[4], faces[5]);
+    }
+    pt_id flatten(Flattener &f) const override
+    {
+        pt_id id[6];
+        for (int i = 0; i < 6; i++) id[i] = f.image(faces[i]);
+        return ptCheck(pt_tex_skybox(f.s, id[0], id[1], id[2], id[3], id[4], id[5]));
+    }
+    Image faces[6];
+};
+
+class ImageSkyboxAlphaTexture : public Texture /* image_texture.h:117-181 */
+{
+public:
+    ImageSkyboxAlphaTexture(Image top, Image bottom, Image left, Image right, Image front, Image back)
+        : faces{top, bottom, left, right, front, back}
+    {
+    }
+    Texture *duplicate() const override
+    {
+        return new ImageSkyboxAlphaTexture(faces[0], faces[1], faces[2], faces[3], faces[4], faces[5]);
+    }
+    pt_id flatten(Flattener &f) const override
+    {
+        pt_id id[6];
+        for (int i = 0; i < 6; i++) id[i] = f.image(faces[i]);
+        return ptCheck(pt_tex_skybox_alpha(f.s, id[0], id[1], id[2], id[3], id[4], id[5]));
+    }
+    Image faces[6];
+};
+
+/* owning single-child wrappers: FilterTexture (filter_texture.h:8-28) and
+ * TransformTexture (transform_texture.h:8-31) */
+class WrapTexture : public Texture
+{
+public:
+    explicit WrapTexture(Texture *t) : t(t) {}
+    ~WrapTexture() override { delete t; }
+
+protected:
+    Texture *const t;
+};
+
+class MultiplyTexture : public WrapTexture /* filter_texture.h:30-48 */
+{
+public:
+    MultiplyTexture(Color factor, Texture *t) : WrapTexture(t), factor(factor) {}
+    Texture *duplicate() const override { return new MultiplyTexture(factor, t->duplicate()); }
+    pt_id flatten(Flattener &f) const override
+    {
+        return ptCheck(pt_tex_multiply(f.s, factor.x, factor.y, factor.z, f.texture(t)));
+    }
+    Color factor;
+};
+
+class LogTexture : public WrapTexture /* filter_texture.h:50-80 */
+{
+public:
+    explicit LogTexture(Texture *t) : WrapTexture(t) {}
+    Texture *duplicate() const override { return new LogTexture(t->duplicate()); }
+    pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_log(f.s, f.texture(t))); }
+};
+
+class MirrorBallSkymapTexture : public WrapTexture /* transform_texture.h:33-59 */
+{
+public:
+    explicit MirrorBallSkymapTexture(Texture *t) : WrapTexture(t) {}
+    Texture *duplicate() const override { return new MirrorBallSkymapTexture(t->duplicate()); }
+    pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_mirrorball(f.s, f.texture(t))); }
+};
+
+class SphericalCoordinatesSkymapTexture : public WrapTexture /* :61-85 */
+{
+public:
+    explicit SphericalCoordinatesSkymapTexture(Texture *t) : WrapTexture(t) {}
+    Texture *duplicate() const override { return new SphericalCoordinatesSkymapTexture(t->duplicate()); }
+    pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_spherical(f.s, f.texture(t))); }
+};
+
+/* --------------------------------------------------------------- material -- */
+struct Material /* include/material.h:10-37 */
+{
+    Texture *reflect;
+    Texture *scatter_coefficient;
+    Texture *emissive;
+    Texture *transmit;
+    float ior;
+    Texture *transmit_reflect_coefficient;
+    Material(Texture *reflect = new ColorTexture(1), Texture *scatter_coefficient = new ColorTexture(1),
+             Texture *emissive = new ColorTexture(0), Texture *transmit = new ColorTexture(0), float ior = 1,
+             Texture *transmit_reflect_coefficient = new ColorTexture(0))
+        : reflect(reflect), scatter_coefficient(scatter_coefficient), emissive(emissive), transmit(transmit),
+          ior(ior), transmit_reflect_coefficient(transmit_reflect_coefficient)
+    {
+    }
+    ~Material()
+    {
+        delete reflect;
+        delete scatter_coefficient;
+        delete emissive;
+        delete transmit;
+        delete transmit_reflect_coefficient;
+    }
+    Material *duplicate() const
+    {
+        return new Material(reflect->duplicate(), scatter_coefficient->duplicate(), emissive->duplicate(),
+                            transmit->duplicate(), ior, transmit_reflect_coefficient->duplicate());
+    }
+    Material(const Material &) = delete;
+    Material &operator=(const Material &) = delete;
+};
+
+inline Material *transform(const Matrix &m, const Material *mat) /* material.h:39-43 */
+{
+    return new Material(transform(m, mat->reflect), transform(m, mat->scatter_coefficient),
+                        transform(m, mat->emissive), transform(m, mat->transmit), mat->ior,
+                        transform(m, mat->transmit_reflect_coefficient));
+}
+
+inline pt_id Flattener::texture(const Texture *t)
+{
+    auto it = textures_.find(t);
+    if (it != textures_.end())
+        return it->second;
+    pt_id id = t->flatten(*this);
+    return textures_[t] = id;
+}
+
+inline pt_id Flattener::material(const Material *m)
+{
+    if (!m)
+        throw std::invalid_argument("null material"); /* path-trace.h:77 asserts it */
+    auto it = materials_.find(m);
+    if (it != materials_.end())
+        return it->second;
+    pt_id id = ptCheck(pt_material(s, texture(m->reflect), texture(m->scatter_coefficient), texture(m->emissive),
+                                   texture(m->transmit), m->ior, texture(m->transmit_reflect_coefficient)));
+    return materials_[m] = id;
+}
+
+/* ----------------------------------------------------------------- objects -- */
+class Object /* include/object.h:10-24 */
+{
+public:
+    virtual ~Object() {}
+    virtual Object *transform(const Matrix &) const { return nullptr; }
+    virtual Object *duplicate() const = 0;
+    virtual pt_id flatten(Flattener &f) const = 0;
+};
+
+class TransformedObject : public Object /* object.h:26-98 */
+{
+public:
+    TransformedObject(const Matrix &m, Object *o) : m(m), o(o) {}
+    ~TransformedObject() override { delete o; }
+    Object *transform(const Matrix &m2) const override { return new TransformedObject(m.concat(m2), o->duplicate()); }
+    Object *duplicate() const override { return new TransformedObject(m, o->duplicate()); }
+    pt_id flatten(Flattener &f) const override
+    {
+        float a[12];
+        m.get(a);
+        return ptCheck(pt_transformed(f.s, a, o->flatten(f)));
+    }
+
+private:
+    Matrix m;
+    Object *o;
+};
+
+inline Object *transform(const Matrix &m, Object *o) /* object.h:100-106 */
+{
+    Object *r = o->transform(m);
+    return r ? r : new TransformedObject(m, o->duplicate());
+}
+
+class Sphere : public Object /* include/sphere.h, src/sphere.cpp */
+{
+public:
+    Sphere(Vector3D center, float r, const Material *material) : center(center), r(r), material(material) {}
+    Object *duplicate() const override { return new Sphere(center, r, material); }
+    pt_id flatten(Flattener &f) const override
+    {
+        return ptCheck(pt_sphere(f.s, center.x, center.y, center.z, r, f.material(material)));
+    }
+
+private:
+    Vector3D center;
+    float r;
+    const Material *material;
+};
+
+class Plane : public Object /* include/plane.h, src/plane.cpp:6-14 */
+{
+public:
+    Plane(Vector3D normal, float d, const Material *material) : normal(normal), d(d), material(material) {}
+    Plane(Vector3D normal, Vector3D pos, const Material *material)
+        : normal(normal), d(-dot(normal, pos)), material(material)
+    {
+    }
+    Object *duplicate() const override { return new Plane(normal, d, material); }
+    pt_id flatten(Flattener &f) const override
+    {
+        return ptCheck(pt_plane(f.s, normal.x, normal.y, normal.z, d, f.material(material)));
+    }
+
+private:
+    Vector3D normal;
+    float d;
+    const Material *material;
+};
+
+template <class Self, int OP>
+class CsgObject : public Object
+{
+public:
+    CsgObject(Object *a, Object *b) : a(a), b(b) {}
+    ~CsgObject() override
+    {
+        delete a;
+        delete b;
+    }
+    Object *duplicate() const override { return new Self(a->duplicate(), b->duplicate()); }
+    /* union.h:21, intersection.h:21, difference.h:21 transform `a` twice (the
+     * second operand is dropped) -- kept so that transformed scenes match. */
+    Object *transform(const Matrix &m) const override
+    {
+        return new Self(PathTrace::transform(m, a), PathTrace::transform(m, a));
+    }
+    pt_id flatten(Flattener &f) const override
+    {
+        pt_id ia = a->flatten(f);
+        pt_id ib = b->flatten(f);
+        return ptCheck(pt_csg(f.s, OP, ia, ib));
+    }
+
+private:
+    Object *const a;
+    Object *const b;
+};
+
+class Union : public CsgObject<Union, PT_CSG_UNION> /* include/union.h, src/union.cpp */
+{
+public:
+    using CsgObject::CsgObject;
+};
+class Intersection : public CsgObject<Intersection, PT_CSG_INTERSECTION> /* src/intersection.cpp */
+{
+public:
+    using CsgObject::CsgObject;
+};
+class Difference : public CsgObject<Difference, PT_CSG_DIFFERENCE> /* src/difference.cpp */
+{
+public:
+    using CsgObject::CsgObject;
+};
+
+inline Object *unionArray(Object *array[], int start, int end) /* src/test.cpp:52-64 */
+{
+    if (end - start == 1)
+        return array[start];
+    if (end - start == 2)
+        return new Union(array[start], array[start + 1]);
+    int split = (end - start) / 2 + start;
+    return new Union(unionArray(array, start, split), unionArray(array, split, end));
+}
+
+/* ---------------------------------------------------------------- renderer -- */
+/* Replaces world->makeSpanIterator() + tracePixel<T> per pixel.  The object
+ * graph is flattened once; the Renderer does not keep pointers into it. */
+class Renderer
+{
+public:
+    struct Settings
+    {
+        int width = 0, height = 0;  /* screenXResolution, screenYResolution       */
+        int sampleCount = 1;        /* tracePixel sampleCount                       */
+        int rayDepth = 16;          /* tracePixel/traceRay depth                    */
+        float screenWidth = 0, screenHeight = 0, screenDistance = 0; /* 0 = the demo's
+                                       convention: W, H, 2 min(W, H) (src/test.cpp:450) */
+        uint64_t seed = 0x5EED;     /* run seed of the per-(pixel, sample) engine   */
+        int order = PT_ORDER_GROUP64;
+        int device = 0;
+        int64_t maxBufferBytes = 0;
+    };
+
+    explicit Renderer(const Object *world) : s_(pt_scene_create())
+    {
+        if (!s_)
+            throw DeviceError(PT_ERR_DEVICE, pt_last_error());
+        try {
+            Flattener f(s_);
+            ptCheck(pt_set_root(s_, world->flatten(f)));
+        } catch (...) {
+            pt_scene_destroy(s_);
+            throw;
+        }
+    }
+    ~Renderer() { pt_scene_destroy(s_); }
+    Renderer(const Renderer &) = delete;
+    Renderer &operator=(const Renderer &) = delete;
+
+    pt_scene *handle() const { return s_; }
+
+    /* Mean radiance per pixel (tracePixel's return value), row-major, for the
+     * whole frame -- or, with pixels != nullptr, for those pixel indices. */
+    std::vector<Color> render(const Settings &st, const int32_t *pixels = nullptr, int64_t npixels = 0,
+                              pt_render_stats *stats = nullptr) const
+    {
+        pt_render_params p = params(st, pixels, npixels);
+        int64_t n = pixels ? npixels : (int64_t)st.width * st.height;
+        std::vector<Color> out((size_t)n);
+        static_assert(sizeof(Color) == 3 * sizeof(float), "Color must be 3 packed floats");
+        ptCheck(pt_render(s_, &p, reinterpret_cast<float *>(out.data()), stats));
+        return out;
+    }
+
+    /* Device-side variant: fb is a W*H*3 float device buffer, stream a hipStream_t. */
+    void renderDevice(const Settings &st, float *fb, void *stream, const int32_t *pixels = nullptr,
+                      int64_t npixels = 0, pt_render_stats *stats = nullptr) const
+    {
+        pt_render_params p = params(st, pixels, npixels);
+        ptCheck(pt_render_device(s_, &p, fb, stream, stats));
+    }
+
+    /* Compile / upload everything a render with these settings needs. */
+    void prepare(const Settings &st) const
+    {
+        pt_render_params p = params(st, nullptr, 0);
+        ptCheck(pt_prepare(s_, &p));
+    }
+
+    static pt_render_params params(const Settings &st, const int32_t *pixels, int64_t npixels)
+    {
+        pt_render_params p;
+        p.width = st.width, p.height = st.height, p.spp = st.sampleCount, p.depth = st.rayDepth;
+        const float dmin = (float)(st.width < st.height ? st.width : st.height);
+        p.screen_w = st.screenWidth > 0 ? st.screenWidth : (float)st.width;
+        p.screen_h = st.screenHeight > 0 ? st.screenHeight : (float)st.height;
+        p.screen_dist = st.screenDistance > 0 ? st.screenDistance : 2 * dmin;
+        p.seed = st.seed, p.order = st.order, p.device = st.device;
+        p.pixels = pixels, p.npixels = npixels, p.max_buffer_bytes = st.maxBufferBytes;
+        return p;
+    }
+
+private:
+    pt_scene *s_;
+};
+
+/* SDL_SaveBMP of the demo's tone map (src/test.cpp:1037-1059). */
+inline void writeBMP(const std::string &path, const std::vector<Color> &rgb, int w, int h, int count = 1)
+{
+    if (pt_write_bmp(path.c_str(), reinterpret_cast<const float *>(rgb.data()), w, h, count) != PT_OK)
+        throw ImageStoreError(pt_last_error());
+}
+
+} // namespace PathTrace
+
+#endif
