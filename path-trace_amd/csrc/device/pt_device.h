@@ -115,10 +115,12 @@ __device__ __forceinline__ float sqrt_core(float x)
     s = (ru > 0.0f) ? su : s;
     return s;
 }
-__device__ __forceinline__ float csqrt(float x) /* == __builtin_sqrtf(x), bitwise */
+/* sqrt_core alone is exact for x >= 2^-96 (incl. +inf), x == +-0 and NaN. */
+__device__ __forceinline__ bool sqrt_core_ok(float x) { return !(x < 0x1p-96f) || x == 0.0f; }
+__device__ __forceinline__ float csqrt(float x) /* == __builtin_sqrtf(x), bitwise (checked by the self-test) */
 {
     float s = sqrt_core(x);
-    if (!(x >= 0x1p-96f && x <= 0x1.fffffep127f))
+    if (!sqrt_core_ok(x))
         s = __builtin_sqrtf(x);
     return s;
 }
@@ -165,14 +167,31 @@ __device__ __forceinline__ float cdiv(float n, const Rcp &R, bool dok)
         q = n / R.d;
     return q;
 }
+/* True on every lane when any active lane has p: a scalar (wave-uniform)
+ * branch, so a rarely needed slow path costs one compare-and-branch instead
+ * of exec-mask bookkeeping or an if-converted second evaluation. */
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
+
+
 __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
 {
-    float m = csqrt(dot(v, v));
+    const float x = dot(v, v);
+    float m = sqrt_core(x);
+    const bool sbad = !sqrt_core_ok(x);
+    if (wave_any(sbad)) {
+        if (sbad)
+            m = __builtin_sqrtf(x);
+    }
     if (m == 0.0f)
         m = 1.0f;
     Rcp R = mkrcp(m);
-    bool dok = den_ok(m);
-    return mk(cdiv(v.x, R, dok), cdiv(v.y, R, dok), cdiv(v.z, R, dok));
+    V3 q = mk(div_core(v.x, R), div_core(v.y, R), div_core(v.z, R));
+    const bool dbad = !(den_ok(m) && num_ok(v.x) && num_ok(v.y) && num_ok(v.z));
+    if (wave_any(dbad)) {
+        if (dbad)
+            q = mk(v.x / m, v.y / m, v.z / m);
+    }
+    return q;
 }
 /* (int)x as x86 cvttss2si: out-of-range and NaN give INT_MIN (the reference
  * runs on x86; v_cvt_i32_f32 would saturate / give 0). */
@@ -333,7 +352,28 @@ __device__ __forceinline__ void end_from_start(CS &a, const CS &b) { a.t1 = b.t0
 __device__ __forceinline__ void start_from_end(CS &a, const CS &b) { a.t0 = b.t1, a.r0 = b.r1 ^ FLIP; }
 __device__ __forceinline__ void start_from_start(CS &a, const CS &b) { a.t0 = b.t0, a.r0 = b.r0; }
 
-/* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r. */
+/* One query direction as every primitive of a traversal sees it: |d|^2 and
+ * its refined reciprocal are shared (the sphere quotients all divide by a). */
+struct Ray
+{
+    V3 d;
+    float a;
+    Rcp ra;
+    int aok; /* den_ok(a) */
+};
+__device__ __forceinline__ Ray mkray(V3 d)
+{
+    Ray q;
+    q.d = d;
+    q.a = dot(d, d);
+    q.ra = mkrcp(q.a);
+    q.aok = den_ok(q.a) ? 1 : 0;
+    return q;
+}
+
+/* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r.  Branch-free:
+ * t0/t1 are computed on every lane (dead lanes' values are never read), with
+ * one wave-uniform fallback for operands outside the exact fast paths. */
 template <int PRIM, int OFF, int MAT>
 struct Sph
 {
@@ -353,18 +393,21 @@ struct Sph
         c.omc = univ(o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
         c.c = unif(dot(c.omc, c.omc) - e.P[OFF + 3]);
     }
-    __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float a, const Env &)
+    __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &)
     {
-        float b = dot(c.omc, d);
-        float disc = b * b - a * c.c;
-        s.live = !(disc <= EPS) ? 1 : 0;
-        if (s.live) {
-            float q = csqrt(disc);
-            Rcp R = mkrcp(a);
-            bool dok = den_ok(a);
-            s.t0 = cdiv(-b - q, R, dok);
-            s.t1 = cdiv(-b + q, R, dok);
+        const float b = dot(c.omc, q.d);
+        const float disc = b * b - q.a * c.c;
+        const bool live = !(disc <= EPS);
+        const float sq = sqrt_core(disc); /* exact: disc > EPS (or inf/NaN) where live */
+        const float n0 = -b - sq, n1 = -b + sq;
+        float t0 = div_core(n0, q.ra), t1 = div_core(n1, q.ra);
+        const bool bad = live && !(q.aok && num_ok(n0) && num_ok(n1));
+        if (wave_any(bad)) {
+            if (bad)
+                t0 = n0 / q.a, t1 = n1 / q.a;
         }
+        s.live = live ? 1 : 0;
+        s.t0 = t0, s.t1 = t1;
     }
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
@@ -399,25 +442,21 @@ struct Pln
     {
         c.num = unif(-e.P[OFF + 3] - dot(o, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2])));
     }
-    __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float, const Env &e)
+    __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)
     {
-        float div = dot(d, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
-        float t = 0.0f;
-        bool deg = __builtin_fabsf(div) < EPS * EPS;
-        if (!deg) {
-            t = c.num / div;
-            deg = __builtin_fabsf(t) >= MAXV;
+        const float div = dot(q.d, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+        const bool small = __builtin_fabsf(div) < EPS * EPS;
+        float t = div_core(c.num, mkrcp(div));
+        const bool bad = !small && !(den_ok(div) && num_ok(c.num));
+        if (wave_any(bad)) {
+            if (bad)
+                t = c.num / div;
         }
-        if (deg) {
-            s.live = __builtin_fabsf(c.num) < EPS * EPS ? 1 : 0;
-            s.t0 = -MAXV, s.t1 = MAXV;
-        } else if (div < 0.0f) {
-            s.live = 1;
-            s.t0 = t, s.t1 = MAXV;
-        } else {
-            s.live = 1;
-            s.t0 = -MAXV, s.t1 = t;
-        }
+        const bool deg = small || __builtin_fabsf(t) >= MAXV;
+        const bool neg = div < 0.0f;
+        s.live = (!deg || __builtin_fabsf(c.num) < EPS * EPS) ? 1 : 0;
+        s.t0 = (!deg && neg) ? t : -MAXV;
+        s.t1 = (!deg && !neg) ? t : MAXV;
     }
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
@@ -456,10 +495,10 @@ struct Pln
         A::prep(c.a, o, e);                                                                         \
         B::prep(c.b, o, e);                                                                         \
     }                                                                                               \
-    __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float a, const Env &e) \
+    __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)   \
     {                                                                                               \
-        A::init(s.a, c.a, d, a, e);                                                                 \
-        B::init(s.b, c.b, d, a, e);                                                                 \
+        A::init(s.a, c.a, q, e);                                                                    \
+        B::init(s.b, c.b, q, e);                                                                    \
         s.ea = !A::pull(s.a, s.sa);                                                                 \
         s.eb = !B::pull(s.b, s.sb);                                                                 \
     }                                                                                               \
@@ -606,10 +645,9 @@ struct Xf
     };
     typedef typename C::St St;
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e) { C::prep(c.c, univ(m_apply(e.P + MOFF, o)), e); }
-    __device__ static __forceinline__ void init(St &s, const Ctx &c, V3 d, float, const Env &e)
+    __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)
     {
-        V3 dl = m_lin(e.P + MOFF, d);
-        C::init(s, c.c, dl, dot(dl, dl), e);
+        C::init(s, c.c, mkray(m_lin(e.P + MOFF, q.d)), e);
     }
     __device__ static __forceinline__ bool pull(St &s, CS &out) { return C::pull(s, out); }
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)
@@ -625,7 +663,7 @@ __device__ __forceinline__ bool first_hit(const typename R::Ctx &ctx, V3 d, cons
                                           bool &exit_hit)
 {
     typename R::St st;
-    R::init(st, ctx, d, dot(d, d), e);
+    R::init(st, ctx, mkray(d), e);
     CS s;
     while (R::pull(st, s)) {
         if (s.t0 >= MAXV)
@@ -883,16 +921,121 @@ struct Frame
 
 enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 
+#define PT_QCAP 256 /* leaf-child ring per wave: < 64 queued + 128 accepted per round */
+
+/* One rejection attempt of the scatter loop body (path-trace.h:141-158):
+ * draws s0, s1, s2 are the attempt's three engine states. */
+struct Attempt
+{
+    V3 wn;         /* accepted direction (unnormalised in deferred mode)      */
+    float factor;  /* 1 - (1 - dot(wn, n)) * sc (0 in deferred mode)         */
+    int acc, fail, nonleaf;
+};
+
+template <bool DEFERRED>
+__device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float sc, float sNa, float abs_rc,
+                                           bool child_leaf_depth)
+{
+    const u64 s1 = s0 * PCG_MULT + inc;
+    const u64 s2 = s1 * PCG_MULT + inc;
+    const V3 v = mk(u11(pcg_out(s0)), u11(pcg_out(s1)), u11(pcg_out(s2)));
+    /* rand(): while (mag > max) with mag = sqrt(|v|^2); correctly rounded
+     * sqrt(x) > 1  <=>  x > 1 + 2^-23 (exhaustively checked) */
+    const bool ball = !(dot(v, v) > 0x1.000002p+0f);
+    const V3 w = v + kR;
+    const bool hemi = !(dot(n, w) <= EPS); /* while (dot(normal, dir) <= eps) */
+    Attempt a;
+    a.acc = (ball && hemi) ? 1 : 0;
+    a.fail = (ball && !hemi) ? 1 : 0;
+    a.wn = w;
+    a.factor = 0.0f;
+    a.nonleaf = 0;
+    if (!DEFERRED) {
+        a.wn = cnormalize(w);
+        a.factor = 1.0f - (1.0f - dot(a.wn, n)) * sc;
+        const float cs = (sNa * a.factor) * abs_rc;
+        a.nonleaf = (a.acc && !(child_leaf_depth || cs < EPS)) ? 1 : 0;
+    }
+    return a;
+}
+
+/* Replays the reference's sequential consumption of one half-round of 64
+ * attempts (attempt j of the half = lane j) given its accept / hemisphere-
+ * fail / non-leaf masks.  rem = children still to generate.  Returns the last
+ * consumed attempt (63 when the whole half is consumed and no stop occurs);
+ * sets `reason` on a stop and `take` = accepted leaf attempts consumed. */
+__device__ __forceinline__ int replay(u64 A, u64 F, u64 NL, int rem, int &fails, int &reason, u64 &take)
+{
+    const int pa = __popcll(A), pf = __popcll(F);
+    if (NL == 0ull && pa < rem && fails + pf < 1000) {
+        /* common case: every attempt of the half is consumed */
+        take = A;
+        if (A) {
+            const int last = 63 - __builtin_clzll(A);
+            fails = (last == 63) ? 0 : __popcll(F >> (last + 1));
+        } else {
+            fails += pf;
+        }
+        return 63;
+    }
+    const int nl = NL ? __builtin_ctzll(NL) : 64;
+    const int pos_rem = (pa >= rem) ? nth_set_bit(A, rem) : 64;
+    int pos_abort = 64;
+    if (fails + pf >= 1000) {
+        int fc = fails;
+        for (int l = 0; l < 64; l++) {
+            if (l == nl || l == pos_rem)
+                break;
+            if ((A >> l) & 1ull)
+                fc = 0;
+            else if ((F >> l) & 1ull) {
+                if (++fc == 1000) {
+                    pos_abort = l;
+                    break;
+                }
+            }
+        }
+    }
+    if (pos_abort < 64 && pos_abort < nl && pos_abort < pos_rem) {
+        reason = B_ABORT;
+        take = A & ((1ull << pos_abort) - 1ull);
+        return pos_abort;
+    }
+    if (nl < 64 && nl <= pos_rem) {
+        reason = B_NONLEAF;
+        take = A & ((1ull << nl) - 1ull);
+        return nl;
+    }
+    if (pos_rem < 64) {
+        reason = B_DONE;
+        take = (pos_rem == 63) ? A : (A & ((2ull << pos_rem) - 1ull));
+        return pos_rem;
+    }
+    take = A;
+    if (A) {
+        const int last = 63 - __builtin_clzll(A);
+        fails = (last == 63) ? 0 : __popcll(F >> (last + 1));
+    } else {
+        fails += pf;
+    }
+    return 63;
+}
+
 /* Wave-cooperative scatter loop (path-trace.h:138-163) for sc > eps, from
- * child index f.i.  Returns B_DONE when all N children are summed, B_ABORT on
- * the reference's count > 1000 early return (path-trace.h:149-152), B_NONLEAF
- * after writing the next child's ray into `child` when that child must
- * recurse (it draws random numbers, so it runs on the spine). */
-template <class S, bool STRICT>
-__device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
-                                     float4 *q, Frame &f, Frame &child, Counters &cnt)
+ * child index f.i.  Each generation round evaluates 128 consecutive rejection
+ * attempts, two per lane (attempts l and 64 + l: draws 3l.. and 192 + 3l..),
+ * replays the sequential rule on the ballots, and queues accepted leaf
+ * children; every 64 queued children are traced one per lane.  Returns
+ * B_DONE when all N children are summed, B_ABORT on the reference's
+ * count > 1000 early return (path-trace.h:149-152), B_NONLEAF after writing
+ * the next child's ray into `child` when that child must recurse (it draws
+ * random numbers, so it runs on the spine). */
+template <class S, bool STRICT, bool DEFERRED>
+__device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
+                                       float4 *q, Frame &f, Frame &child, Counters &cnt)
 {
     const int lane = threadIdx.x & 63;
+    const u64 below = (1ull << lane) - 1ull;
     const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
     const float sc = unif(f.sc), strength = unif(f.strength), add = unif(f.add);
     const int depth = uni(f.depth), N = uni(f.N);
@@ -903,111 +1046,65 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
     const float aN = unif(add / (float)N);                /* addFactor / scatter_ray_count                       */
     const float abs_rc = unif(length(rc));
     const bool child_leaf_depth = depth - 1 <= 0;
-    /* Every child is provably a leaf when depth-1 <= 0 or when even the largest
-     * possible factor (1 + 4e-7: wn and n are unit vectors) keeps the child
-     * strength below eps.  Then acceptance needs no normalisation, and the
-     * normalised direction / factor are computed per child at trace time
-     * (same arithmetic, same bits) with every lane busy. */
-    const bool deferred = child_leaf_depth || (sNa * abs_rc * 1.01f < EPS);
     const u64 ginc = G3l * rng.inc;
-    const u64 A64 = jump[128], G64 = jump[129]; /* full round: 192 draws */
+    const u64 A64 = jump[128], g64inc = jump[129] * rng.inc;   /* 64 attempts = 192 draws  */
+    const u64 A128 = jump[256], g128inc = jump[257] * rng.inc; /* 128 attempts = 384 draws */
     int qhead = 0, qn = 0, fails = 0, reason = -1;
-    u64 n_rounds = 0, n_att = 0, n_leaf = 0;
+    u32 n_rounds = 0, n_att = 0, n_leaf = 0;
     for (;;) {
         if (reason < 0 && qn < 64) {
-            /* ---- generation round: lane l evaluates attempt l (draws 3l..3l+2) */
-            const int rem = N - (i + qn);
-            u64 s0 = A3l * rng.st + ginc;
-            u64 s1 = s0 * PCG_MULT + rng.inc;
-            u64 s2 = s1 * PCG_MULT + rng.inc;
-            V3 v = mk(u11(pcg_out(s0)), u11(pcg_out(s1)), u11(pcg_out(s2)));
-            /* rand(): while (mag > max) with mag = sqrt(|v|^2); correctly rounded
-             * sqrt(x) > 1  <=>  x > 1 + 2^-23 (exhaustively checked) */
-            bool ball = !(dot(v, v) > 0x1.000002p+0f);
-            V3 w = v + kR;
-            bool hemi = !(dot(n, w) <= EPS);                 /* while (dot(normal, dir) <= eps) */
-            bool acc = ball && hemi;
-            V3 wn = w;
-            float factor = 0.0f;
-            bool leaf = true;
-            if (!deferred && acc) {
-                wn = cnormalize(w);
-                factor = 1.0f - (1.0f - dot(wn, n)) * sc;
-                float cs = (sNa * factor) * abs_rc;
-                leaf = child_leaf_depth || cs < EPS;
-            }
-            const u64 A = __ballot(acc), F = __ballot(ball && !hemi);
-            const u64 NL = deferred ? 0ull : __ballot(acc && !leaf);
+            /* ---- generation round: lane l evaluates attempts l and 64 + l */
+            const u64 sa = A3l * rng.st + ginc;
+            const u64 sb = A64 * sa + g64inc;
+            const Attempt a0 = attempt<DEFERRED>(sa, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
+            const Attempt a1 = attempt<DEFERRED>(sb, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
+            const u64 A0 = __ballot(a0.acc), F0 = __ballot(a0.fail), NL0 = DEFERRED ? 0ull : __ballot(a0.nonleaf);
+            const u64 A1 = __ballot(a1.acc), F1 = __ballot(a1.fail), NL1 = DEFERRED ? 0ull : __ballot(a1.nonleaf);
             n_rounds++;
             /* ---- replay the sequential consumption rule on the masks */
-            const int nl = NL ? __builtin_ctzll(NL) : 64;
-            const int pos_rem = (__popcll(A) >= (unsigned)rem) ? nth_set_bit(A, rem) : 64;
-            int pos_abort = 64;
-            if (fails + __popcll(F) >= 1000) {
-                int fc = fails;
-                for (int l = 0; l < 64; l++) {
-                    if (l == nl || l == pos_rem)
-                        break;
-                    if ((A >> l) & 1ull)
-                        fc = 0;
-                    else if ((F >> l) & 1ull) {
-                        if (++fc == 1000) {
-                            pos_abort = l;
-                            break;
-                        }
-                    }
-                }
+            const int rem = N - (i + qn);
+            u64 take0 = 0, take1 = 0;
+            int m; /* attempts consumed this round, 1..128 */
+            const int c0 = replay(A0, F0, NL0, rem, fails, reason, take0);
+            if (reason >= 0) {
+                m = c0 + 1;
+            } else {
+                const int c1 = replay(A1, F1, NL1, rem - __popcll(A0), fails, reason, take1);
+                m = 64 + c1 + 1;
             }
-            int cut = 63;
-            u64 take; /* accepted leaf attempts consumed this round */
-            if (pos_abort < 64 && pos_abort < nl && pos_abort < pos_rem) {
-                reason = B_ABORT, cut = pos_abort;
-                take = A & ((1ull << cut) - 1ull);
-            } else if (nl < 64 && nl <= pos_rem) {
-                reason = B_NONLEAF, cut = nl;
-                take = A & ((1ull << cut) - 1ull);
-                V3 nd = mk(rdlane(wn.x, nl), rdlane(wn.y, nl), rdlane(wn.z, nl));
-                float nf = rdlane(factor, nl);
+            if (!DEFERRED && reason == B_NONLEAF) {
+                const int l = (m - 1) & 63;
+                const Attempt &an = (m > 64) ? a1 : a0;
+                const V3 nd = mk(rdlane(an.wn.x, l), rdlane(an.wn.y, l), rdlane(an.wn.z, l));
+                const float nf = rdlane(an.factor, l);
                 /* w = addFactor / N * factor * reflect; strength = strength / N * addFactor * factor * |reflect| */
                 f.w = (aN * nf) * rc;
                 child.o = hit;
                 child.d = nd;
                 child.strength = (sNa * nf) * abs_rc;
                 child.depth = depth - 1;
-            } else if (pos_rem < 64) {
-                reason = B_DONE, cut = pos_rem;
-                take = (cut == 63) ? A : (A & ((2ull << cut) - 1ull));
-            } else {
-                take = A;
-                if (A) {
-                    int last = 63 - __builtin_clzll(A);
-                    fails = (last == 63) ? 0 : __popcll(F >> (last + 1));
-                } else {
-                    fails += __popcll(F);
-                }
             }
-            n_att += (u64)(cut + 1);
-            if ((take >> lane) & 1ull) {
-                int r = __popcll(take & ((1ull << lane) - 1ull));
-                q[(qhead + qn + r) & 127] = make_float4(wn.x, wn.y, wn.z, factor);
-            }
-            qn += __popcll(take);
+            n_att += (u32)m;
+            const int base0 = qhead + qn, base1 = base0 + __popcll(take0);
+            if ((take0 >> lane) & 1ull)
+                q[(base0 + __popcll(take0 & below)) & (PT_QCAP - 1)] = make_float4(a0.wn.x, a0.wn.y, a0.wn.z, a0.factor);
+            if ((take1 >> lane) & 1ull)
+                q[(base1 + __popcll(take1 & below)) & (PT_QCAP - 1)] = make_float4(a1.wn.x, a1.wn.y, a1.wn.z, a1.factor);
+            qn += __popcll(take0) + __popcll(take1);
             /* ---- advance the sample's stream past the consumed attempts */
-            if (cut == 63) {
-                rng.st = A64 * rng.st + G64 * rng.inc;
-            } else {
-                const int m = cut + 1;
+            if (m == 128)
+                rng.st = A128 * rng.st + g128inc;
+            else
                 rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
-            }
         }
         if (qn >= 64 || (reason >= 0 && qn > 0)) {
             /* ---- trace one batch of leaf children, one per lane */
             const int cntb = qn < 64 ? qn : 64;
             V3 term = mk(-0.0f, -0.0f, -0.0f);
             if (lane < cntb) {
-                float4 en = q[(qhead + lane) & 127];
+                float4 en = q[(qhead + lane) & (PT_QCAP - 1)];
                 V3 dir = mk(en.x, en.y, en.z);
-                if (deferred) {
+                if (DEFERRED) {
                     dir = cnormalize(dir);
                     en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
                 }
@@ -1027,7 +1124,7 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
                 /* experiment: primitive tests without CSG merges */
                 {
                     typename S::Root::St st;
-                    S::Root::init(st, ctx, dir, dot(dir, dir), e);
+                    S::Root::init(st, ctx, mkray(dir), e);
                     t = st.sa.t0 + st.sb.t0;
                     col = S::emis(0, hit + t * dir, e);
                 }
@@ -1044,7 +1141,7 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
                 retval = retval + mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
                 retval = univ(retval);
             }
-            n_leaf += (u64)cntb;
+            n_leaf += (u32)cntb;
             qhead += cntb;
             qn -= cntb;
             i += cntb;
@@ -1059,6 +1156,23 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
     cnt.attempts += n_att;
     cnt.leaf += n_leaf;
     return reason;
+}
+
+/* Every child is provably a leaf when depth-1 <= 0 or when even the largest
+ * possible factor (1 + 4e-7: wn and n are unit vectors) keeps the child
+ * strength below eps.  Then acceptance needs no normalisation, and the
+ * normalised direction / factor are computed per child at trace time (same
+ * arithmetic, same bits) with every lane busy. */
+template <class S, bool STRICT>
+__device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
+                                     float4 *q, Frame &f, Frame &child, Counters &cnt)
+{
+    const float sNa = unif((unif(f.strength) / (float)uni(f.N)) * unif(f.add));
+    const float abs_rc = unif(length(univ(f.rc)));
+    const bool deferred = uni(f.depth) - 1 <= 0 || (sNa * abs_rc * 1.01f < EPS);
+    if (deferred)
+        return burst_t<S, STRICT, true>(e, rng, jump, A3l, G3l, q, f, child, cnt);
+    return burst_t<S, STRICT, false>(e, rng, jump, A3l, G3l, q, f, child, cnt);
 }
 
 enum { PH_ENTER, PH_SETUP, PH_LOOP, PH_RETURN };
@@ -1229,7 +1343,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                                              const PtLaunch &lp)
 {
     __shared__ Frame stk[PT_WPW][MAXD + 1];
-    __shared__ float4 qbuf[PT_WPW][128];
+    __shared__ float4 qbuf[PT_WPW][PT_QCAP];
     __shared__ Counters cbuf[PT_WPW];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const Env e = {P, imgs};

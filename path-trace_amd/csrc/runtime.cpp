@@ -400,11 +400,11 @@ void load_text(SceneImpl &s, const std::string &text)
     s.root = root;
 }
 
-/* jump table (A_{3m}, G_{3m}), m = 0..64, of state_{n+3m} = A*state_n + G*inc */
+/* jump table (A_{3m}, G_{3m}), m = 0..128, of state_{n+3m} = A*state_n + G*inc */
 std::vector<uint64_t> jump_table()
 {
-    std::vector<uint64_t> t(2 * 65);
-    for (uint32_t m = 0; m <= 64; m++) pt_pcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
+    std::vector<uint64_t> t(2 * 129);
+    for (uint32_t m = 0; m <= 128; m++) pt_pcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
     return t;
 }
 
