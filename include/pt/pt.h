@@ -128,6 +128,7 @@ typedef struct pt_render_stats {
     uint64_t attempts;             /* rejection attempts evaluated (64 per round)               */
     uint64_t rounds;               /* attempt rounds                                            */
     uint64_t sphere_tests, sphere_hits, plane_tests;
+    uint64_t slow_queries;         /* leaf children that needed the full CSG merge (slow pass)  */
 } pt_render_stats;
 
 /* Synchronous: renders the frame into rgb_out (host memory), which receives,

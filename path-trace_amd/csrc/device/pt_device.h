@@ -371,6 +371,35 @@ __device__ __forceinline__ Ray mkray(V3 d)
     return q;
 }
 
+/* ---- fast first-hit ----------------------------------
+ * Every primitive contributes at most one span.  When every pair of spans that
+ * meets at a merge node (x from the node's A side, y from its B side, each a
+ * "positive" primitive of that side: one reachable through Union children,
+ * Difference A sides and TransformedObjects, not through an Intersection) is
+ * either strictly separated or lies entirely before EPS, the lazy merges pass
+ * every positive span through unchanged apart from spans ending before EPS,
+ * which traceRay's scan skips.  The first qualifying span of the root is then
+ * the live positive span with t1 >= EPS and the smallest t0, and the scan's
+ * tests (path-trace.h:66-100) apply to it alone.  Lanes that fail the check
+ * take the full merge; both give the same bits. */
+template <int V>
+struct IC
+{
+    static constexpr int value = V;
+};
+template <int NP>
+struct PrimSpans
+{
+    float t0[NP], t1[NP];
+    int live[NP];
+};
+template <class PS>
+__device__ __forceinline__ int sep(const PS &ps, int x, int y)
+{
+    return (!ps.live[x]) | (!ps.live[y]) | (ps.t1[x] < ps.t0[y]) | (ps.t1[y] < ps.t0[x]) |
+           ((ps.t1[x] < EPS) & (ps.t1[y] < EPS));
+}
+
 /* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r.  Branch-free:
  * t0/t1 are computed on every lane (dead lanes' values are never read), with
  * one wave-uniform fallback for operands outside the exact fast paths. */
@@ -418,6 +447,17 @@ struct Sph
         s.live = 0;
         return true;
     }
+    template <class PS>
+    __device__ static __forceinline__ void span(PS &ps, const Ctx &c, const Ray &q, const Env &e)
+    {
+        St s;
+        init(s, c, q, e);
+        ps.t0[PRIM] = s.t0, ps.t1[PRIM] = s.t1, ps.live[PRIM] = s.live;
+    }
+    template <class F>
+    __device__ static __forceinline__ void each_pos(F &&f) { f(IC<PRIM>(), IC<MAT>()); }
+    template <class PS>
+    __device__ static __forceinline__ int fast_ok(const PS &) { return 1; }
     __device__ static __forceinline__ V3 normal(int, float t, V3 o, V3 d, const Env &e)
     {
         return normalize((o + t * d) - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
@@ -467,6 +507,17 @@ struct Pln
         s.live = 0;
         return true;
     }
+    template <class PS>
+    __device__ static __forceinline__ void span(PS &ps, const Ctx &c, const Ray &q, const Env &e)
+    {
+        St s;
+        init(s, c, q, e);
+        ps.t0[PRIM] = s.t0, ps.t1[PRIM] = s.t1, ps.live[PRIM] = s.live;
+    }
+    template <class F>
+    __device__ static __forceinline__ void each_pos(F &&f) { f(IC<PRIM>(), IC<MAT>()); }
+    template <class PS>
+    __device__ static __forceinline__ int fast_ok(const PS &) { return 1; }
     __device__ static __forceinline__ V3 normal(int, float, V3, V3, const Env &e)
     {
         return normalize(mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
@@ -502,6 +553,19 @@ struct Pln
         s.ea = !A::pull(s.a, s.sa);                                                                 \
         s.eb = !B::pull(s.b, s.sb);                                                                 \
     }                                                                                               \
+    template <class PS>                                                                             \
+    __device__ static __forceinline__ void span(PS &ps, const Ctx &c, const Ray &q, const Env &e)  \
+    {                                                                                               \
+        A::span(ps, c.a, q, e);                                                                     \
+        B::span(ps, c.b, q, e);                                                                     \
+    }                                                                                               \
+    template <class PS>                                                                             \
+    __device__ static __forceinline__ int fast_ok(const PS &ps)                                     \
+    {                                                                                               \
+        int ok = A::fast_ok(ps) & B::fast_ok(ps);                                                   \
+        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= sep(ps, decltype(x)::value, decltype(y)::value); }); }); \
+        return ok;                                                                                  \
+    }                                                                                               \
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)       \
     {                                                                                               \
         if (prim < A::HI)                                                                           \
@@ -518,6 +582,12 @@ template <class A, class B>
 struct Uni
 {
     PTD_BINARY_COMMON
+    template <class F>
+    __device__ static __forceinline__ void each_pos(F &&f)
+    {
+        A::each_pos(f);
+        B::each_pos(f);
+    }
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
         for (;;) {
@@ -556,6 +626,8 @@ template <class A, class B>
 struct Isect
 {
     PTD_BINARY_COMMON
+    template <class F>
+    __device__ static __forceinline__ void each_pos(F &&) {}
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
         for (;;) {
@@ -594,6 +666,8 @@ template <class A, class B>
 struct Diff
 {
     PTD_BINARY_COMMON
+    template <class F>
+    __device__ static __forceinline__ void each_pos(F &&f) { A::each_pos(f); }
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
         for (;;) {
@@ -650,6 +724,15 @@ struct Xf
         C::init(s, c.c, mkray(m_lin(e.P + MOFF, q.d)), e);
     }
     __device__ static __forceinline__ bool pull(St &s, CS &out) { return C::pull(s, out); }
+    template <class PS>
+    __device__ static __forceinline__ void span(PS &ps, const Ctx &c, const Ray &q, const Env &e)
+    {
+        C::span(ps, c.c, mkray(m_lin(e.P + MOFF, q.d)), e);
+    }
+    template <class F>
+    __device__ static __forceinline__ void each_pos(F &&f) { C::each_pos(f); }
+    template <class PS>
+    __device__ static __forceinline__ int fast_ok(const PS &ps) { return C::fast_ok(ps); }
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)
     {
         V3 n = C::normal(prim, t, m_apply(e.P + MOFF, o), m_lin(e.P + MOFF, d), e);
@@ -680,6 +763,34 @@ __device__ __forceinline__ bool first_hit(const typename R::Ctx &ctx, V3 d, cons
         }
     }
     return false;
+}
+
+/* Fast first hit over precomputed primitive spans; valid when R::fast_ok. */
+template <class R, class PS>
+__device__ __forceinline__ bool fast_first_hit(const PS &ps, float &t, int &mat)
+{
+    int found = 0, bm = 0;
+    float b0 = 0.0f, b1 = 0.0f;
+    R::each_pos([&](auto x, auto m) {
+        constexpr int X = decltype(x)::value;
+        const int cand = ps.live[X] & (ps.t1[X] >= EPS);
+        const int better = cand & ((!found) | (ps.t0[X] < b0));
+        b0 = better ? ps.t0[X] : b0;
+        b1 = better ? ps.t1[X] : b1;
+        bm = better ? decltype(m)::value : bm;
+        found |= cand;
+    });
+    mat = bm;
+    if (!found || b0 >= MAXV)
+        return false;
+    if (b0 >= EPS) {
+        t = b0;
+        return true;
+    }
+    if (b1 >= MAXV)
+        return false;
+    t = b1;
+    return true;
 }
 
 /* ------------------------------------------------------------ textures --- */
@@ -895,7 +1006,15 @@ struct TSpherical
 /* Per-wave statistics, kept in LDS (every lane writes the same value). */
 struct Counters
 {
-    u64 queries, leaf, attempts, rounds, shaded, nonleaf;
+    u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow;
+};
+
+/* Per-wave LDS work areas of the scatter loop. */
+struct WaveLds
+{
+    float4 *q;    /* PT_QCAP queued leaf-child rays (direction, factor)        */
+    float4 *ring; /* PT_RCAP child slots: parked ray, then the child's term   */
+    int *slowq;   /* PT_SCAP slot positions waiting for the full merge        */
 };
 
 /* ---------------------------------------------------------------- spine --- */
@@ -921,7 +1040,14 @@ struct Frame
 
 enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 
-#define PT_QCAP 256 /* leaf-child ring per wave: < 64 queued + 128 accepted per round */
+#ifndef PT_KATT
+#define PT_KATT 2 /* rejection attempts per lane per generation round */
+#endif
+#define PT_QCAP 256 /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
+#define PT_RCAP 256 /* child slots per wave awaiting their group sum               */
+#define PT_SCAP 128 /* parked children per wave: < 64 + one fast pass               */
+static_assert(64 + 64 * PT_KATT <= PT_QCAP, "queue too small for PT_KATT");
+#define PT_JUMP_ENTRIES 193 /* host table: m = 0..192 attempts (PT_KATT <= 3) */
 
 /* One rejection attempt of the scatter loop body (path-trace.h:141-158):
  * draws s0, s1, s2 are the attempt's three engine states. */
@@ -1022,8 +1148,9 @@ __device__ __forceinline__ int replay(u64 A, u64 F, u64 NL, int rem, int &fails,
 }
 
 /* Wave-cooperative scatter loop (path-trace.h:138-163) for sc > eps, from
- * child index f.i.  Each generation round evaluates 128 consecutive rejection
- * attempts, two per lane (attempts l and 64 + l: draws 3l.. and 192 + 3l..),
+ * child index f.i.  Each generation round evaluates 64*PT_KATT consecutive
+ * rejection attempts, PT_KATT per lane (attempts l, 64 + l, ..: draws 3l..,
+ * 192 + 3l.., ..),
  * replays the sequential rule on the ballots, and queues accepted leaf
  * children; every 64 queued children are traced one per lane.  Returns
  * B_DONE when all N children are summed, B_ABORT on the reference's
@@ -1032,8 +1159,10 @@ __device__ __forceinline__ int replay(u64 A, u64 F, u64 NL, int rem, int &fails,
  * random numbers, so it runs on the spine). */
 template <class S, bool STRICT, bool DEFERRED>
 __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
-                                       float4 *q, Frame &f, Frame &child, Counters &cnt)
+                                       const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
+    float4 *const q = L.q, *const ring = L.ring;
+    int *const slowq = L.slowq;
     const int lane = threadIdx.x & 63;
     const u64 below = (1ull << lane) - 1ull;
     const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
@@ -1048,35 +1177,51 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const bool child_leaf_depth = depth - 1 <= 0;
     const u64 ginc = G3l * rng.inc;
     const u64 A64 = jump[128], g64inc = jump[129] * rng.inc;   /* 64 attempts = 192 draws  */
-    const u64 A128 = jump[256], g128inc = jump[257] * rng.inc; /* 128 attempts = 384 draws */
+    const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * rng.inc; /* a full round */
     int qhead = 0, qn = 0, fails = 0, reason = -1;
-    u32 n_rounds = 0, n_att = 0, n_leaf = 0;
+    int npos = 0, sum_ptr = 0, s_head = 0, s_n = 0; /* slot ring / slow queue positions */
+    u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0;
     for (;;) {
         if (reason < 0 && qn < 64) {
-            /* ---- generation round: lane l evaluates attempts l and 64 + l */
-            const u64 sa = A3l * rng.st + ginc;
-            const u64 sb = A64 * sa + g64inc;
-            const Attempt a0 = attempt<DEFERRED>(sa, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
-            const Attempt a1 = attempt<DEFERRED>(sb, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
-            const u64 A0 = __ballot(a0.acc), F0 = __ballot(a0.fail), NL0 = DEFERRED ? 0ull : __ballot(a0.nonleaf);
-            const u64 A1 = __ballot(a1.acc), F1 = __ballot(a1.fail), NL1 = DEFERRED ? 0ull : __ballot(a1.nonleaf);
+            /* ---- generation round: lane l evaluates attempts l, 64 + l, ... */
+            Attempt at[PT_KATT];
+            u64 Am[PT_KATT], Fm[PT_KATT], NLm[PT_KATT];
+            {
+                u64 sk = A3l * rng.st + ginc;
+#pragma unroll
+                for (int k = 0; k < PT_KATT; k++) {
+                    if (k)
+                        sk = A64 * sk + g64inc;
+                    at[k] = attempt<DEFERRED>(sk, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
+                    Am[k] = __ballot(at[k].acc);
+                    Fm[k] = __ballot(at[k].fail);
+                    NLm[k] = DEFERRED ? 0ull : __ballot(at[k].nonleaf);
+                }
+            }
             n_rounds++;
             /* ---- replay the sequential consumption rule on the masks */
-            const int rem = N - (i + qn);
-            u64 take0 = 0, take1 = 0;
-            int m; /* attempts consumed this round, 1..128 */
-            const int c0 = replay(A0, F0, NL0, rem, fails, reason, take0);
-            if (reason >= 0) {
-                m = c0 + 1;
-            } else {
-                const int c1 = replay(A1, F1, NL1, rem - __popcll(A0), fails, reason, take1);
-                m = 64 + c1 + 1;
+            int rem = N - (i + qn);
+            u64 take[PT_KATT];
+            int m = 0; /* attempts consumed this round, 1..64*PT_KATT */
+#pragma unroll
+            for (int k = 0; k < PT_KATT; k++) {
+                take[k] = 0ull;
+                if (reason < 0) {
+                    const int c = replay(Am[k], Fm[k], NLm[k], rem, fails, reason, take[k]);
+                    m = 64 * k + c + 1;
+                    rem -= __popcll(Am[k]);
+                }
             }
             if (!DEFERRED && reason == B_NONLEAF) {
-                const int l = (m - 1) & 63;
-                const Attempt &an = (m > 64) ? a1 : a0;
-                const V3 nd = mk(rdlane(an.wn.x, l), rdlane(an.wn.y, l), rdlane(an.wn.z, l));
-                const float nf = rdlane(an.factor, l);
+                const int l = (m - 1) & 63, kk = (m - 1) >> 6;
+                V3 wn = at[0].wn;
+                float fac = at[0].factor;
+#pragma unroll
+                for (int k = 1; k < PT_KATT; k++)
+                    if (kk == k)
+                        wn = at[k].wn, fac = at[k].factor;
+                const V3 nd = mk(rdlane(wn.x, l), rdlane(wn.y, l), rdlane(wn.z, l));
+                const float nf = rdlane(fac, l);
                 /* w = addFactor / N * factor * reflect; strength = strength / N * addFactor * factor * |reflect| */
                 f.w = (aN * nf) * rc;
                 child.o = hit;
@@ -1085,22 +1230,27 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 child.depth = depth - 1;
             }
             n_att += (u32)m;
-            const int base0 = qhead + qn, base1 = base0 + __popcll(take0);
-            if ((take0 >> lane) & 1ull)
-                q[(base0 + __popcll(take0 & below)) & (PT_QCAP - 1)] = make_float4(a0.wn.x, a0.wn.y, a0.wn.z, a0.factor);
-            if ((take1 >> lane) & 1ull)
-                q[(base1 + __popcll(take1 & below)) & (PT_QCAP - 1)] = make_float4(a1.wn.x, a1.wn.y, a1.wn.z, a1.factor);
-            qn += __popcll(take0) + __popcll(take1);
+            int base = qhead + qn;
+#pragma unroll
+            for (int k = 0; k < PT_KATT; k++) {
+                if ((take[k] >> lane) & 1ull)
+                    q[(base + __popcll(take[k] & below)) & (PT_QCAP - 1)] =
+                        make_float4(at[k].wn.x, at[k].wn.y, at[k].wn.z, at[k].factor);
+                base += __popcll(take[k]);
+            }
+            qn = base - qhead;
             /* ---- advance the sample's stream past the consumed attempts */
-            if (m == 128)
-                rng.st = A128 * rng.st + g128inc;
+            if (m == 64 * PT_KATT)
+                rng.st = Afull * rng.st + gfullinc;
             else
                 rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
         }
         if (qn >= 64 || (reason >= 0 && qn > 0)) {
-            /* ---- trace one batch of leaf children, one per lane */
+            /* ---- fast pass: one queued leaf child per lane.  Lanes whose spans
+             * pass the fast check finish here and leave their term in the slot
+             * ring; the others leave their ray there and queue for a slow pass. */
             const int cntb = qn < 64 ? qn : 64;
-            V3 term = mk(-0.0f, -0.0f, -0.0f);
+            int slow = 0;
             if (lane < cntb) {
                 float4 en = q[(qhead + lane) & (PT_QCAP - 1)];
                 V3 dir = mk(en.x, en.y, en.z);
@@ -1108,46 +1258,90 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     dir = cnormalize(dir);
                     en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
                 }
+                float4 out;
+#if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
+                /* experiment: generation cost only */
+                {
+                    const V3 col = dir.z < 0.0f ? S::emis(0, hit + dir, e) : mk(0, 0, 0);
+                    const V3 term = ((aN * en.w) * rc) * col;
+                    out = make_float4(term.x, term.y, term.z, 0.0f);
+                }
+#else
+                typename S::Root::Ctx ctx;
+                S::Root::prep(ctx, hit, e);
+                PrimSpans<S::Root::HI> ps;
+                S::Root::span(ps, ctx, mkray(dir), e);
+                if (S::Root::fast_ok(ps)) {
+                    float t = 0.0f;
+                    int mat = 0;
+                    V3 col = mk(0, 0, 0);
+                    if (fast_first_hit<typename S::Root>(ps, t, mat))
+                        col = S::emis(mat, hit + t * dir, e);
+                    const V3 term = ((aN * en.w) * rc) * col;
+                    out = make_float4(term.x, term.y, term.z, 0.0f);
+                } else {
+                    slow = 1;
+                    out = make_float4(dir.x, dir.y, dir.z, en.w);
+                }
+#endif
+                ring[(npos + lane) & (PT_RCAP - 1)] = out;
+            }
+            const u64 SM = __ballot(slow);
+            if (slow)
+                slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = npos + lane;
+            s_n += __popcll(SM);
+            npos += cntb;
+            n_leaf += (u32)cntb;
+            n_slow += (u32)__popcll(SM);
+            qhead += cntb;
+            qn -= cntb;
+            i += cntb;
+        }
+        const bool final = reason >= 0 && qn == 0;
+        /* ---- slow passes: 64 parked children at a time through the full merge,
+         * when 64 are waiting, the slot ring is filling up, or at the end */
+        while (s_n > 0 && (s_n >= 64 || final || npos - sum_ptr > PT_RCAP - 64)) {
+            const int cs = s_n < 64 ? s_n : 64;
+            if (lane < cs) {
+                const int pos = slowq[(s_head + lane) & (PT_SCAP - 1)];
+                const float4 en = ring[pos & (PT_RCAP - 1)];
+                const V3 dir = mk(en.x, en.y, en.z);
                 typename S::Root::Ctx ctx;
                 S::Root::prep(ctx, hit, e);
                 float t;
                 u32 ref;
                 bool ex;
                 V3 col = mk(0, 0, 0);
-#if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
-                /* experiment: generation cost only */
-                if (dir.z < 0.0f) {
-                    t = 1.0f, ref = 0u;
-                    col = S::emis(0, hit + t * dir, e);
-                }
-#elif defined(PT_LEAF_STUB) && PT_LEAF_STUB == 2
-                /* experiment: primitive tests without CSG merges */
-                {
-                    typename S::Root::St st;
-                    S::Root::init(st, ctx, mkray(dir), e);
-                    t = st.sa.t0 + st.sb.t0;
-                    col = S::emis(0, hit + t * dir, e);
-                }
-#else
                 if (first_hit<typename S::Root>(ctx, dir, e, t, ref, ex))
                     col = S::emis(ref_mat(ref), hit + t * dir, e);
-#endif
-                term = ((aN * en.w) * rc) * col;
+                const V3 term = ((aN * en.w) * rc) * col;
+                ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
             }
-            if (STRICT) {
-                for (int j = 0; j < cntb; j++)
-                    retval = retval + mk(rdlane(term.x, j), rdlane(term.y, j), rdlane(term.z, j));
-            } else {
-                retval = retval + mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
-                retval = univ(retval);
-            }
-            n_leaf += (u32)cntb;
-            qhead += cntb;
-            qn -= cntb;
-            i += cntb;
-            continue;
+            s_head += cs;
+            s_n -= cs;
         }
-        if (reason >= 0)
+        /* ---- sum finished groups in order: 64 children per group (the last
+         * group of a burst may be shorter), group-64 tree or sequential */
+        {
+            const int resolved = s_n ? uni(slowq[s_head & (PT_SCAP - 1)]) : npos;
+            while (sum_ptr < resolved && (resolved - sum_ptr >= 64 || (final && s_n == 0))) {
+                const int cg = (npos - sum_ptr) < 64 ? (npos - sum_ptr) : 64;
+                V3 term = mk(-0.0f, -0.0f, -0.0f);
+                if (lane < cg) {
+                    const float4 tv = ring[(sum_ptr + lane) & (PT_RCAP - 1)];
+                    term = mk(tv.x, tv.y, tv.z);
+                }
+                if (STRICT) {
+                    for (int j = 0; j < cg; j++)
+                        retval = retval + mk(rdlane(term.x, j), rdlane(term.y, j), rdlane(term.z, j));
+                } else {
+                    retval = retval + mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
+                    retval = univ(retval);
+                }
+                sum_ptr += cg;
+            }
+        }
+        if (final)
             break;
     }
     f.retval = retval;
@@ -1155,6 +1349,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     cnt.rounds += n_rounds;
     cnt.attempts += n_att;
     cnt.leaf += n_leaf;
+    cnt.slow += n_slow;
     return reason;
 }
 
@@ -1165,14 +1360,14 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
  * arithmetic, same bits) with every lane busy. */
 template <class S, bool STRICT>
 __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
-                                     float4 *q, Frame &f, Frame &child, Counters &cnt)
+                                     const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
     const float sNa = unif((unif(f.strength) / (float)uni(f.N)) * unif(f.add));
     const float abs_rc = unif(length(univ(f.rc)));
     const bool deferred = uni(f.depth) - 1 <= 0 || (sNa * abs_rc * 1.01f < EPS);
     if (deferred)
-        return burst_t<S, STRICT, true>(e, rng, jump, A3l, G3l, q, f, child, cnt);
-    return burst_t<S, STRICT, false>(e, rng, jump, A3l, G3l, q, f, child, cnt);
+        return burst_t<S, STRICT, true>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+    return burst_t<S, STRICT, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
 }
 
 enum { PH_ENTER, PH_SETUP, PH_LOOP, PH_RETURN };
@@ -1181,7 +1376,7 @@ enum { RS_REFRACT, RS_SCATTER };
 /* One sample = one traceRay tree (path-trace.h:58-165) + the jittered camera
  * ray of tracePixel (path-trace.h:190-198).  F = this wave's frame stack. */
 template <class S, int MAXD, bool STRICT>
-__device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, float4 *q,
+__device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, const WaveLds &L,
                                            const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt)
 {
     Rng rng;
@@ -1281,7 +1476,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 continue;
             }
             if (unif(f.sc) > EPS) {
-                int why = burst<S, STRICT>(e, rng, jump, A3l, G3l, q, f, F[sp + 1], cnt);
+                int why = burst<S, STRICT>(e, rng, jump, A3l, G3l, L, f, F[sp + 1], cnt);
                 if (why != B_NONLEAF) {
                     result = univ(f.retval);
                     phase = PH_RETURN;
@@ -1344,12 +1539,15 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
 {
     __shared__ Frame stk[PT_WPW][MAXD + 1];
     __shared__ float4 qbuf[PT_WPW][PT_QCAP];
+    __shared__ float4 rbuf[PT_WPW][PT_RCAP];
+    __shared__ int sbuf[PT_WPW][PT_SCAP];
     __shared__ Counters cbuf[PT_WPW];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const Env e = {P, imgs};
     const u64 A3l = jump[2 * lane], G3l = jump[2 * lane + 1];
     Counters &cnt = cbuf[wave];
-    cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = 0;
+    cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = cnt.slow = 0;
+    const WaveLds L = {qbuf[wave], rbuf[wave], sbuf[wave]};
     const long long n_chunks = (lp.n_items + PT_CHUNK - 1) / PT_CHUNK;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
     for (;;) {
@@ -1368,7 +1566,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             const long long slot = item / lp.nsamp;
             const int s = lp.s0 + (int)(item - slot * lp.nsamp);
             const int pix = pixels ? pixels[slot] : (int)slot;
-            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], qbuf[wave], jump, A3l, G3l,
+            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], L, jump, A3l, G3l,
                                                  cnt);
             if (lane == j)
                 mine = c;
@@ -1387,6 +1585,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         atomicAdd(&stats[3], cnt.rounds);
         atomicAdd(&stats[4], cnt.shaded);
         atomicAdd(&stats[5], cnt.nonleaf);
+        atomicAdd(&stats[6], cnt.slow);
     }
 }
 

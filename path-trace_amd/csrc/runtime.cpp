@@ -400,11 +400,12 @@ void load_text(SceneImpl &s, const std::string &text)
     s.root = root;
 }
 
-/* jump table (A_{3m}, G_{3m}), m = 0..128, of state_{n+3m} = A*state_n + G*inc */
+/* jump table (A_{3m}, G_{3m}), m = 0..192, of state_{n+3m} = A*state_n + G*inc
+ * (PT_JUMP_ENTRIES of the device code: up to 3 x 64 attempts per round) */
 std::vector<uint64_t> jump_table()
 {
-    std::vector<uint64_t> t(2 * 129);
-    for (uint32_t m = 0; m <= 128; m++) pt_pcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
+    std::vector<uint64_t> t(2 * 193);
+    for (uint32_t m = 0; m <= 192; m++) pt_pcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
     return t;
 }
 
@@ -619,6 +620,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
         st->leaf_queries = c[1];
         st->attempts = c[2];
         st->rounds = c[3];
+        st->slow_queries = c[6];
         st->sphere_tests = st->queries * (uint64_t)g.n_spheres;
         st->plane_tests = st->queries * (uint64_t)g.n_planes;
         for (auto e : evs) (void)hipEventDestroy(e);

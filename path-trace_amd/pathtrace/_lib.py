@@ -33,7 +33,8 @@ class RenderStats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("reduce_ms", ctypes.c_double), ("launches", ctypes.c_uint64),
                 ("samples", ctypes.c_uint64), ("queries", ctypes.c_uint64), ("leaf_queries", ctypes.c_uint64),
                 ("attempts", ctypes.c_uint64), ("rounds", ctypes.c_uint64), ("sphere_tests", ctypes.c_uint64),
-                ("sphere_hits", ctypes.c_uint64), ("plane_tests", ctypes.c_uint64)]
+                ("sphere_hits", ctypes.c_uint64), ("plane_tests", ctypes.c_uint64),
+                ("slow_queries", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
