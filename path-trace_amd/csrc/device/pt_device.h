@@ -1180,6 +1180,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * rng.inc; /* a full round */
     int qhead = 0, qn = 0, fails = 0, reason = -1;
     int npos = 0, sum_ptr = 0, s_head = 0, s_n = 0; /* slot ring / slow queue positions */
+    int fast_on = 1;
     u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0;
     for (;;) {
         if (reason < 0 && qn < 64) {
@@ -1259,6 +1260,11 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
                 }
                 float4 out;
+                if (!fast_on) {
+                    /* the fast check keeps failing in this burst: park every child */
+                    slow = 1;
+                    out = make_float4(dir.x, dir.y, dir.z, en.w);
+                } else {
 #if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
                 /* experiment: generation cost only */
                 {
@@ -1280,13 +1286,23 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     const V3 term = ((aN * en.w) * rc) * col;
                     out = make_float4(term.x, term.y, term.z, 0.0f);
                 } else {
+#if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 3
+                    /* experiment: fast pass only (slow lanes contribute 0) */
+                    out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#else
                     slow = 1;
                     out = make_float4(dir.x, dir.y, dir.z, en.w);
+#endif
                 }
 #endif
+                }
                 ring[(npos + lane) & (PT_RCAP - 1)] = out;
             }
             const u64 SM = __ballot(slow);
+            /* scenes whose spans overlap almost everywhere (e.g. a box of sky
+             * half-spaces) skip the fast pass for the rest of the burst */
+            if (fast_on && 4 * __popcll(SM) > 3 * cntb)
+                fast_on = 0;
             if (slow)
                 slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = npos + lane;
             s_n += __popcll(SM);

@@ -94,8 +94,11 @@ def scene_c2(env_w: int = 640, env_h: int = 480):
     env = procedural_env(env_w, env_h)
     sky = Material(ColorTexture(0), ColorTexture(0),
                    MultiplyTexture((1, 1, 1), MirrorBallSkymapTexture(ImageTexture(env))))
+    # the demo's material mix (src/test.cpp:109-118) minus matBrightDiffuseWhite:
+    # its reflectance 8 makes a child's strength grow at every bounce, so the
+    # ray tree of a sample bouncing near it explodes exponentially
     mats = [m["diffuse"], m["mirror"], m["glass"], m["diffuse"], m["diamond"], m["mirror"], m["glass"],
-            m["brightDiffuse"]]
+            m["diffuse"]]
     objs = []
     for k in range(8):
         ang = 2 * math.pi * k / 8

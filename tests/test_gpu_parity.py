@@ -92,6 +92,23 @@ def test_full_1080p_frame_on_sampled_pixels(built, tmp_path):
     assert 300 < st["queries"] / st["samples"] < 2000
 
 
+@pytest.mark.parametrize("name,spp,npix", [("C1", 4, 2000), ("C2", 2, 300), ("C5", 2, 2000)])
+def test_benchmark_configs_on_sampled_pixels(built, tmp_path, name, spp, npix):
+    """The other benchmark workloads: C1 (P0), C2 (mirror-ball
+    env, depth 16, half-space sky box -- every leaf takes the full merge) and
+    C5 (demo world, lens = Intersection, TransformedTexture, skybox, 4K):
+    the full frame on the GPU, hashed pixels bit for bit against the oracle."""
+    cfg = scenes.CONFIGS[name]
+    root = cfg.scene()
+    img, st = pt.render(root, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
+    assert st["samples"] == cfg.width * cfg.height * spp
+    rng = np.random.default_rng(11)
+    pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
+    o = O.render(to_text(root, str(tmp_path)), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen,
+                 pixels=pix, order=O.ORDER_GROUP64)
+    assert_bits(img.reshape(-1, 3)[pix], o, "%s sample" % name)
+
+
 def test_multipass_equals_single_pass(built):
     """Sample passes bounded by max_buffer_bytes carry the running sums exactly."""
     root = scenes.scene_p1()
