@@ -1053,11 +1053,13 @@ static_assert(64 + 64 * PT_KATT <= PT_QCAP, "queue too small for PT_KATT");
  * draws s0, s1, s2 are the attempt's three engine states. */
 struct Attempt
 {
-    V3 wn;         /* accepted direction (unnormalised in deferred mode)      */
-    float factor;  /* 1 - (1 - dot(wn, n)) * sc (0 in deferred mode)         */
-    int acc, fail, nonleaf;
+    V3 wn;        /* accepted direction (unnormalised in deferred mode)      */
+    float factor; /* 1 - (1 - dot(wn, n)) * sc (0 in deferred mode)         */
+    u64 A, F, NL; /* wave ballots: accepted, hemisphere-failed, non-leaf    */
 };
 
+/* The predicates are balloted where they are produced, so they never pass
+ * through a per-lane integer. */
 template <bool DEFERRED>
 __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float sc, float sNa, float abs_rc,
                                            bool child_leaf_depth)
@@ -1071,16 +1073,16 @@ __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float s
     const V3 w = v + kR;
     const bool hemi = !(dot(n, w) <= EPS); /* while (dot(normal, dir) <= eps) */
     Attempt a;
-    a.acc = (ball && hemi) ? 1 : 0;
-    a.fail = (ball && !hemi) ? 1 : 0;
+    a.A = __ballot(ball && hemi);
+    a.F = __ballot(ball && !hemi);
     a.wn = w;
     a.factor = 0.0f;
-    a.nonleaf = 0;
+    a.NL = 0ull;
     if (!DEFERRED) {
         a.wn = cnormalize(w);
         a.factor = 1.0f - (1.0f - dot(a.wn, n)) * sc;
         const float cs = (sNa * a.factor) * abs_rc;
-        a.nonleaf = (a.acc && !(child_leaf_depth || cs < EPS)) ? 1 : 0;
+        a.NL = __ballot(ball && hemi && !(child_leaf_depth || cs < EPS));
     }
     return a;
 }
@@ -1194,9 +1196,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     if (k)
                         sk = A64 * sk + g64inc;
                     at[k] = attempt<DEFERRED>(sk, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
-                    Am[k] = __ballot(at[k].acc);
-                    Fm[k] = __ballot(at[k].fail);
-                    NLm[k] = DEFERRED ? 0ull : __ballot(at[k].nonleaf);
+                    Am[k] = at[k].A;
+                    Fm[k] = at[k].F;
+                    NLm[k] = at[k].NL;
                 }
             }
             n_rounds++;
