@@ -35,6 +35,18 @@ sys.path[:0] = [os.path.join(ROOT, "path-trace_amd"), os.path.join(ROOT, "oracle
 VALU_PEAK_TOPS = 78.6  # 256 CU x 128 FP32 lanes/clk x 2.4 GHz, no FMA (contraction off for parity)
 # SURVEY.md s8(d) op model calibrated by tools/calibrate_ops.py C3 8192 32 (oracle event counts)
 OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75}
+# HBM bytes per sample of the render kernel from the PMC passes of this same
+# command (tools/pmc_traffic.sh; FETCH_SIZE + WRITE_SIZE, gfx950-corrected)
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "round1", "traffic_C3.json")
+
+
+def traffic_per_launch(samples_per_launch: int):
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+        return round(t["bytes_per_sample"] * samples_per_launch)
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def parse():
@@ -149,8 +161,11 @@ def main():
         if opq:
             ops_per_launch = opq * queries / (args.steps * launches_per_step * world)
             achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12
+            samples_per_launch = W * H * spp // (launches_per_step * world)
             out["roofline"] = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS,
-                               "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+                               "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                               "traffic": traffic_per_launch(samples_per_launch) if cfg.name == "C3" else None,
+                               "traffic_unit": "bytes/launch (PMC, %s)" % os.path.relpath(TRAFFIC_JSON, ROOT),
                                "kernel": "pt_render_fast", "avg_launch_ms": round(kernel_ms, 2),
                                "ops_per_query": opq}
         if not args.no_cpu and world == 1:
