@@ -693,6 +693,22 @@ public:
         ptCheck(pt_render_device(s_, &p, fb, stream, stats));
     }
 
+    /* The demo's adaptive image formation, RenderBlock::renderSquare
+     * (src/test.cpp:423-507): 0 selects the demo's block size, interpolation
+     * limit and colour threshold.  Returns the width*height image. */
+    std::vector<Color> renderAdaptive(const Settings &st, int blockSize = 0, int maxInterp = 0, float minDelta = 0,
+                                      pt_adaptive_params *info = nullptr, pt_render_stats *stats = nullptr) const
+    {
+        pt_render_params p = params(st, nullptr, 0);
+        pt_adaptive_params ap = {};
+        ap.block_size = blockSize, ap.max_interp = maxInterp, ap.min_delta = minDelta;
+        std::vector<Color> out((size_t)st.width * st.height);
+        ptCheck(pt_render_adaptive(s_, &p, &ap, reinterpret_cast<float *>(out.data()), stats));
+        if (info)
+            *info = ap;
+        return out;
+    }
+
     /* Compile / upload everything a render with these settings needs. */
     void prepare(const Settings &st) const
     {
@@ -702,7 +718,7 @@ public:
 
     static pt_render_params params(const Settings &st, const int32_t *pixels, int64_t npixels)
     {
-        pt_render_params p;
+        pt_render_params p = {};
         p.width = st.width, p.height = st.height, p.spp = st.sampleCount, p.depth = st.rayDepth;
         const float dmin = (float)(st.width < st.height ? st.width : st.height);
         p.screen_w = st.screenWidth > 0 ? st.screenWidth : (float)st.width;

@@ -116,6 +116,9 @@ typedef struct pt_render_params {
                                       NULL = all pixels                                         */
     int64_t npixels;               /* length of pixels                                          */
     int64_t max_buffer_bytes;      /* per-sample staging budget (0 = 8 GiB)                     */
+    int grid_width;                /* pixel index = y * grid_width + x (0 = width); > width
+                                      addresses pixels past the right / bottom edge, as the
+                                      adaptive caller's block edges do                          */
 } pt_render_params;
 
 typedef struct pt_render_stats {
@@ -139,10 +142,32 @@ typedef struct pt_render_stats {
 int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_stats *stats);
 
 /* Device variant: writes W*H*3 floats into device memory fb (full frame,
- * row-major; pixels not listed in params->pixels are left untouched) on the
+ * row-major; with params->pixels, 3 floats at 3*index for every listed index,
+ * so fb must cover the largest one; other pixels are left untouched) on the
  * given hipStream_t (NULL = default stream) and returns once the work is
  * enqueued... or completed when stats != NULL (stats need the timings). */
 int pt_render_device(pt_scene *s, const pt_render_params *p, float *fb, void *stream, pt_render_stats *stats);
+
+/* The reference demo's image-formation policy, RenderBlock::renderSquare
+ * (src/test.cpp:423-507): per block of block_size x block_size pixels, trace
+ * the corners, then recursively either interpolate a square (size <=
+ * max_interp and all six corner pairs within min_delta: colorCloseEnough,
+ * :437-440, interpolateSquare :423-436) or trace its five subdivision points
+ * and recurse into the quadrants.  Pixels are traced with p->spp samples each,
+ * one GPU batch per subdivision level over all blocks; engine keys use the
+ * grid y * gw + x with gw = ceil(width / block) * block + 1 (block corners
+ * reach past the right edge).  rgb_out receives
+ * the W*H*3 image.  block_size / max_interp <= 0 select the demo's values
+ * (getBlockSize(width / 8), height / 120, :40-50); min_delta <= 0 selects 0.003. */
+typedef struct pt_adaptive_params {
+    int block_size;
+    int max_interp;
+    float min_delta;
+    int64_t traced_pixels;         /* out: pixels traced                                       */
+    int levels;                    /* out: GPU batches                                          */
+} pt_adaptive_params;
+int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_params *ap, float *rgb_out,
+                       pt_render_stats *stats);
 
 /* Everything a render with p needs -- code object loaded, scene parameters
  * and images uploaded, staging buffers allocated -- without rendering, so a

@@ -31,6 +31,7 @@
 #include "scene_text.h"
 
 #include <atomic>
+#include <functional>
 #include <cmath>
 #include <cstring>
 #include <fstream>
@@ -1012,11 +1013,172 @@ extern "C" {
 
 const char *oracle_last_error() { return g_err.c_str(); }
 
+} // extern "C"
+
+namespace oracle
+{
+/* RenderBlock (reference src/test.cpp:324-507) restated depth-first as the
+ * reference runs it: calcPixelColor :441-465, interpolateSquare :423-436,
+ * colorCloseEnough :437-440, renderSquare :466-499, run :501-507,
+ * copyToBuffer :362-374.  tracePixel = spp samples of the per-(pixel, sample)
+ * engine keyed by py * gw + px, gw = ceil(W / block) * block + 1 (block
+ * corners reach past the right edge), summed in order, / spp. */
+struct AdaptiveBlock
+{
+    int x0, y0, S, W, H, maxS;
+    float mcd;
+    std::vector<V3> buf;
+    std::vector<char> valid;
+    std::function<V3(int, int)> trace_pixel;
+    bool in(int x, int y) const { return !(x < x0 || x - x0 > S) && !(y < y0 || y - y0 > S); }
+    size_t at(int x, int y) const { return (size_t)(x - x0) + (size_t)(y - y0) * (S + 1); }
+    void set_pixel(int x, int y, V3 c)
+    {
+        if (!in(x, y))
+            return;
+        buf[at(x, y)] = c;
+        valid[at(x, y)] = 1;
+    }
+    V3 calc(int x, int y)
+    {
+        if (x >= x0 && x <= x0 + S && y >= y0 && y <= y0 + S && valid[at(x, y)])
+            return buf[at(x, y)];
+        V3 r = trace_pixel(x, y);
+        set_pixel(x, y, r);
+        return r;
+    }
+    bool close(V3 a, V3 b) const { return dot(a - b, a - b) <= mcd * mcd * dot(a, a); }
+    void interpolate(int xo, int yo, int size, V3 tl, V3 tr, V3 bl, V3 br)
+    {
+        for (int y = 0; y < size; y++) {
+            float fy = (float)y / size;
+            V3 l = tl + fy * (bl - tl);
+            V3 r = tr + fy * (br - tr);
+            for (int x = 0; x < size; x++) {
+                float fx = (float)x / size;
+                set_pixel(x + xo, y + yo, l + fx * (r - l));
+            }
+        }
+    }
+    void square(int x, int y, int size, V3 tl, V3 tr, V3 bl, V3 br)
+    {
+        if (x > W || y > H)
+            return;
+        if (size <= 1) {
+            set_pixel(x, y, tl);
+            return;
+        }
+        if (close(tl, tr) && close(tl, bl) && close(tl, br) && close(tr, bl) && close(tr, br) && close(bl, br) &&
+            size <= maxS) {
+            interpolate(x, y, size, tl, tr, bl, br);
+            return;
+        }
+        int half = size / 2, cx = x + half, cy = y + half;
+        V3 tc = calc(cx, y);
+        V3 cl = calc(x, cy);
+        V3 cc = calc(cx, cy);
+        V3 cr = calc(x + size, cy);
+        V3 bc = calc(cx, y + size);
+        square(x, y, half, tl, tc, cl, cc);
+        square(cx, y, half, tc, tr, cc, cr);
+        square(x, cy, half, cl, cc, bl, bc);
+        square(cx, cy, half, cc, cr, bc, br);
+    }
+    void run()
+    {
+        V3 tl = calc(x0, y0), tr = calc(x0 + S, y0), bl = calc(x0, y0 + S), br = calc(x0 + S, y0 + S);
+        square(x0, y0, S, tl, tr, bl, br);
+    }
+};
+} // namespace oracle
+
+extern "C" {
+
+/* out: W*H*3; traced (optional): number of tracePixel calls (cache misses) */
+int oracle_render_adaptive(const char *scene_text, int W, int H, int spp, int depth, float sw, float sh, float dist,
+                           uint64_t seed, int block, int max_interp, float min_delta, int threads, int order,
+                           float *out, uint64_t *traced)
+{
+    try {
+        std::unique_ptr<Scene> scene = load_scene(scene_text);
+        const int gw = (W + block - 1) / block * block + 1; /* blocks reach x = ceil(W / block) * block */
+        std::vector<std::pair<int, int>> origins;
+        for (int y0 = 0; y0 < H; y0 += block)
+            for (int x0 = 0; x0 < W; x0 += block) origins.push_back({x0, y0});
+        std::fill(out, out + (size_t)W * H * 3, 0.0f);
+        std::atomic<int> next(0);
+        std::atomic<uint64_t> ntraced(0);
+        std::mutex mu;
+        std::string err;
+        auto worker = [&]() {
+            Tracer<SampleEngine> tr(*scene, order == 1 ? ORDER_GROUP64 : ORDER_REFERENCE);
+            try {
+                for (;;) {
+                    int k = next.fetch_add(1);
+                    if (k >= (int)origins.size())
+                        break;
+                    AdaptiveBlock b;
+                    b.x0 = origins[k].first, b.y0 = origins[k].second, b.S = block, b.W = W, b.H = H;
+                    b.maxS = max_interp, b.mcd = min_delta;
+                    b.buf.assign((size_t)(block + 1) * (block + 1), V3(0, 0, 0));
+                    b.valid.assign((size_t)(block + 1) * (block + 1), 0);
+                    b.trace_pixel = [&](int px, int py) {
+                        const uint64_t p = (uint64_t)py * gw + px;
+                        V3 acc(0, 0, 0);
+                        for (int s = 0; s < spp; s++) {
+                            SampleEngine e(seed, p, (uint64_t)s);
+                            acc = acc + tr.sample(px, py, W, H, depth, sw, sh, dist, e);
+                        }
+                        ntraced++;
+                        return acc / (float)spp;
+                    };
+                    b.run();
+                    for (int y = b.y0; y < b.y0 + block && y < H; y++)
+                        for (int x = b.x0; x < b.x0 + block && x < W; x++)
+                            if (b.valid[b.at(x, y)]) {
+                                V3 c = b.buf[b.at(x, y)];
+                                float *o = out + 3 * ((size_t)y * W + x);
+                                o[0] = c.x, o[1] = c.y, o[2] = c.z;
+                            }
+                }
+            } catch (std::exception &e) {
+                std::lock_guard<std::mutex> g(mu);
+                err = e.what();
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 0; t < (threads < 1 ? 1 : threads); t++) pool.emplace_back(worker);
+        for (auto &t : pool) t.join();
+        if (!err.empty())
+            throw std::runtime_error(err);
+        if (traced)
+            *traced = ntraced.load();
+        return 0;
+    } catch (std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+
 /* stats[0..10]: queries sphere_tests sphere_hits plane_tests merge_steps shaded
  * refract_children scatter_children attempts draws leaf_children */
+int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int depth, float sw, float sh,
+                     float dist, uint64_t seed, const int32_t *pixels, int npx, int threads, int order,
+                     int per_sample, float *out, uint64_t *stats);
+
 int oracle_render(const char *scene_text, int W, int H, int spp, int depth, float sw, float sh, float dist,
                   uint64_t seed, const int32_t *pixels, int npx, int threads, int order, int per_sample, float *out,
                   uint64_t *stats)
+{
+    return oracle_render_gw(scene_text, W, H, W, spp, depth, sw, sh, dist, seed, pixels, npx, threads, order,
+                            per_sample, out, stats);
+}
+
+/* pixel index p = py * gw + px (gw = W, or W + 1 for the adaptive caller) */
+int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int depth, float sw, float sh,
+                     float dist, uint64_t seed, const int32_t *pixels, int npx, int threads, int order,
+                     int per_sample, float *out, uint64_t *stats)
 {
     try {
         std::unique_ptr<Scene> scene = load_scene(scene_text);
@@ -1032,7 +1194,7 @@ int oracle_render(const char *scene_text, int W, int H, int spp, int depth, floa
                     if (k >= npx)
                         break;
                     int p = pixels ? pixels[k] : k;
-                    int px = p % W, py = p / W;
+                    int px = p % gw, py = p / gw;
                     V3 acc(0, 0, 0);
                     for (int s = 0; s < spp; s++) {
                         SampleEngine e(seed, (uint64_t)p, (uint64_t)s);

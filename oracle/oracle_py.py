@@ -51,6 +51,15 @@ def lib():
         L.oracle_spans.restype = ctypes.c_int
         L.oracle_spans.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                    ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+        C = ctypes
+        L.oracle_render_gw.restype = C.c_int
+        L.oracle_render_gw.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                       C.c_float, C.c_uint64, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.c_void_p, C.c_void_p]
+        L.oracle_render_adaptive.restype = C.c_int
+        L.oracle_render_adaptive.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
+                                             C.c_float, C.c_uint64, C.c_int, C.c_int, C.c_float, C.c_int, C.c_int,
+                                             C.c_void_p, C.c_void_p]
         L.oracle_kat.restype = ctypes.c_int
         L.oracle_kat.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         _lib = L
@@ -77,6 +86,36 @@ def render(scene_text: str, W: int, H: int, spp: int, depth: int, screen=None, s
     if stats:
         return out, dict(zip(STAT_NAMES, [int(v) for v in st[:len(STAT_NAMES)]]))
     return out
+
+
+def render_gw(scene_text: str, W: int, H: int, gw: int, pixels, spp: int, depth: int, screen=None,
+              seed: int = 0x5EED, threads: int = 0, order: int = ORDER_REFERENCE):
+    """Per-pixel means for grid indices p = py * gw + px (gw >= W)."""
+    sw, sh, dist = screen if screen is not None else (float(W), float(H), float(2 * min(W, H)))
+    L = lib()
+    px = np.ascontiguousarray(np.asarray(pixels, dtype=np.int32))
+    out = np.zeros((len(px), 3), dtype=np.float32)
+    rc = L.oracle_render_gw(scene_text.encode(), W, H, gw, spp, depth, sw, sh, dist, seed, px.ctypes.data, len(px),
+                            threads or (os.cpu_count() or 1), order, 0, out.ctypes.data, None)
+    if rc != 0:
+        raise RuntimeError("oracle_render_gw: " + L.oracle_last_error().decode())
+    return out
+
+
+def render_adaptive(scene_text: str, W: int, H: int, spp: int, depth: int, block: int, max_interp: int,
+                    min_delta: float = 0.003, screen=None, seed: int = 0x5EED, threads: int = 0,
+                    order: int = ORDER_REFERENCE):
+    """RenderBlock restated depth-first (oracle.cpp AdaptiveBlock): (H x W x 3, traced pixel count)."""
+    sw, sh, dist = screen if screen is not None else (float(W), float(H), float(2 * min(W, H)))
+    L = lib()
+    out = np.zeros((H, W, 3), dtype=np.float32)
+    traced = np.zeros(1, dtype=np.uint64)
+    rc = L.oracle_render_adaptive(scene_text.encode(), W, H, spp, depth, sw, sh, dist, seed, block, max_interp,
+                                  min_delta, threads or (os.cpu_count() or 1), order, out.ctypes.data,
+                                  traced.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("oracle_render_adaptive: " + L.oracle_last_error().decode())
+    return out, int(traced[0])
 
 
 def _parse_spans(buf: bytes, n: int):

@@ -46,7 +46,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
-    cmd = ["hipcc", "-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+    cmd = ["hipcc", "--offload-arch=gfx950", "-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
            "-Wall", "-Wno-unused-result", "-o", LIB + ".tmp"]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     cmd += ["-ldl"]  # hiprtc is dlopen'ed by path (csrc/jit.cpp)

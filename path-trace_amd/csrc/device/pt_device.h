@@ -61,7 +61,9 @@ struct PtLaunch
     int depth;
     int nsamp;          /* samples per pixel slot in this pass                     */
     int s0;             /* first sample index of this pass                         */
-    int pad0, pad1;
+    int gw;             /* pixel index = py * gw + px (gw = W, or W + 1 for the
+                           adaptive caller's block-edge pixels)                   */
+    int pad1;
 };
 
 struct Env
@@ -1399,7 +1401,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
 {
     Rng rng;
     rng_seed(rng, lp.seed, (u64)pix, (u64)s);
-    const int px = pix % lp.W, py = pix / lp.W;
+    const int px = pix % lp.gw, py = pix / lp.gw;
     {
         float x = 2.0f * ((float)px + u01(rng_next(rng))) / (float)lp.W - 1.0f;
         float y = 1.0f - 2.0f * ((float)py + u01(rng_next(rng))) / (float)lp.H;

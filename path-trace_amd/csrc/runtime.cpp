@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -64,7 +65,7 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     int depth;
     int nsamp;
     int s0;
-    int pad0, pad1;
+    int gw, pad1;
 };
 
 template <class T>
@@ -480,11 +481,23 @@ void validate(const pt_render_params *p)
         throw Error(PT_ERR_ARG, "depth must be in [0, 64]");
     if (p->order != PT_ORDER_GROUP64 && p->order != PT_ORDER_REFERENCE)
         throw Error(PT_ERR_ARG, "bad order");
+    if (p->grid_width != 0 && p->grid_width < p->width)
+        throw Error(PT_ERR_ARG, "grid_width must be 0 or >= width");
     if (p->pixels) {
+        const int64_t limit = p->grid_width ? (int64_t)INT32_MAX : (int64_t)p->width * p->height;
         for (int64_t k = 0; k < p->npixels; k++)
-            if (p->pixels[k] < 0 || p->pixels[k] >= p->width * p->height)
+            if (p->pixels[k] < 0 || p->pixels[k] >= limit)
                 throw Error(PT_ERR_ARG, "pixel index out of range");
     }
+}
+
+/* frame-buffer floats a render with p addresses */
+size_t frame_floats(const pt_render_params *p)
+{
+    size_t n = (size_t)p->width * p->height;
+    if (p->pixels)
+        for (int64_t k = 0; k < p->npixels; k++) n = std::max(n, (size_t)p->pixels[k] + 1);
+    return 3 * n;
 }
 
 long long pass_samples(const pt_render_params *p, long long npix)
@@ -562,6 +575,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             lp.depth = p->depth;
             lp.nsamp = nsamp;
             lp.s0 = s0;
+            lp.gw = p->grid_width > 0 ? p->grid_width : p->width;
             const float *Pp = ds.P.p;
             const PtImageDev *ip = ds.imgs.p;
             const uint64_t *jp = ds.jump.p;
@@ -937,7 +951,7 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
         validate(p);
         SceneImpl &sc = S(s);
         HIPCHECK(hipSetDevice(p->device));
-        size_t n = (size_t)p->width * p->height * 3;
+        const size_t n = frame_floats(p);
         DevBuf<float> fb;
         fb.ensure(n);
         struct Free
@@ -957,6 +971,204 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
             for (int64_t k = 0; k < p->npixels; k++)
                 for (int c = 0; c < 3; c++) rgb_out[3 * k + c] = all[3 * (size_t)p->pixels[k] + c];
         }
+        return PT_OK;
+    });
+}
+
+namespace
+{
+/* ---- adaptive caller (reference src/test.cpp:40-50, :324-507) ------------ */
+struct AV /* Color arithmetic of include/vector3d.h, float, no contraction */
+{
+    float x, y, z;
+};
+AV av_add(AV a, AV b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+AV av_sub(AV a, AV b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+AV av_scale(float s, AV a) { return {a.x * s, a.y * s, a.z * s}; } /* operator*(float, V) = V * s */
+float av_abs2(AV a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+
+int demo_block_size(int count) /* getBlockSize, src/test.cpp:40-48 */
+{
+    int r = 1024;
+    while (r > count && r > 4) r /= 2;
+    return r / 4;
+}
+
+/* RenderBlock's (size+1)^2 pixel cache (src/test.cpp:396-422), with the
+ * traced and interpolated pixels kept apart (state 1 / 2): depth-first, a
+ * square left of / above an interpolated neighbour reads that neighbour's
+ * left / top edge before the interpolation overwrites it, so calc must see
+ * the traced value while the image keeps the interpolated one. */
+struct ABlock
+{
+    int x0, y0, S;
+    std::vector<AV> buf;
+    std::vector<char> st; /* 0 unset, 1 traced, 2 interpolated */
+    bool in(int x, int y) const { return x >= x0 && x - x0 <= S && y >= y0 && y - y0 <= S; }
+    size_t at(int x, int y) const { return (size_t)(x - x0) + (size_t)(y - y0) * (S + 1); }
+    bool traced(int x, int y) const { return in(x, y) && st[at(x, y)] == 1; }
+    void set_traced(int x, int y, AV c)
+    {
+        if (in(x, y) && st[at(x, y)] != 2)
+            buf[at(x, y)] = c, st[at(x, y)] = 1;
+    }
+    void set_interp(int x, int y, AV c)
+    {
+        if (in(x, y))
+            buf[at(x, y)] = c, st[at(x, y)] = 2;
+    }
+};
+
+struct ASquare
+{
+    int b, x, y, size;
+    AV tl, tr, bl, br;
+};
+} // namespace
+
+/* One level-synchronous evaluation of renderSquare over every block: the
+ * squares of a level are decided, the points they need are traced in one GPU
+ * batch, then their quadrants form the next level.  With traced and
+ * interpolated pixels kept apart (ABlock), every calcPixelColor sees what it
+ * sees depth-first -- the traced value -- and every interpolation overwrites
+ * as it does depth-first, so the image equals the recursion's (checked
+ * against the oracle's depth-first restatement, tests/test_adaptive.py). */
+int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_params *ap, float *rgb_out,
+                       pt_render_stats *stats)
+{
+    return guard([&] {
+        if (!rgb_out || !ap)
+            throw Error(PT_ERR_ARG, "null output or adaptive params");
+        if (p->pixels)
+            throw Error(PT_ERR_ARG, "adaptive render takes no pixel list");
+        validate(p);
+        (void)S(s);
+        const int W = p->width, H = p->height;
+        const int S = ap->block_size > 0 ? ap->block_size : demo_block_size(W / 8);
+        /* blocks reach x = ceil(W / S) * S: the engine grid is that wide + 1 */
+        const int gw = (W + S - 1) / S * S + 1;
+        const int maxS = ap->max_interp > 0 ? ap->max_interp : H / (480 / 4);
+        const float mcd = ap->min_delta > 0 ? ap->min_delta : 0.003f;
+        if (S <= 0)
+            throw Error(PT_ERR_ARG, "block size must be positive");
+        std::vector<ABlock> blocks;
+        for (int y0 = 0; y0 < H; y0 += S) /* makeBlockRenderer order, src/test.cpp:940-956 */
+            for (int x0 = 0; x0 < W; x0 += S) {
+                ABlock b{x0, y0, S, std::vector<AV>((size_t)(S + 1) * (S + 1)),
+                         std::vector<char>((size_t)(S + 1) * (S + 1), 0)};
+                blocks.push_back(std::move(b));
+            }
+        std::map<int64_t, AV> traced;
+        std::vector<int32_t> need;
+        pt_render_stats acc;
+        memset(&acc, 0, sizeof acc);
+        ap->traced_pixels = 0;
+        ap->levels = 0;
+        auto want = [&](int x, int y) {
+            const int64_t k = (int64_t)y * gw + x;
+            if (k < 0 || k > INT32_MAX)
+                throw Error(PT_ERR_ARG, "adaptive block reaches past the index range");
+            if (traced.emplace(k, AV{0, 0, 0}).second)
+                need.push_back((int32_t)k);
+        };
+        auto flush = [&]() {
+            if (need.empty())
+                return;
+            pt_render_params q = *p;
+            q.pixels = need.data();
+            q.npixels = (int64_t)need.size();
+            q.grid_width = gw;
+            std::vector<float> out(need.size() * 3);
+            pt_render_stats st;
+            int rc = pt_render(s, &q, out.data(), &st);
+            if (rc != PT_OK)
+                throw Error(rc, pt_last_error());
+            for (size_t k = 0; k < need.size(); k++) traced[need[k]] = AV{out[3 * k], out[3 * k + 1], out[3 * k + 2]};
+            acc.kernel_ms += st.kernel_ms, acc.reduce_ms += st.reduce_ms, acc.launches += st.launches;
+            acc.samples += st.samples, acc.queries += st.queries, acc.leaf_queries += st.leaf_queries;
+            acc.attempts += st.attempts, acc.rounds += st.rounds, acc.slow_queries += st.slow_queries;
+            ap->traced_pixels += (int64_t)need.size();
+            ap->levels++;
+            need.clear();
+        };
+        /* calcPixelColor (src/test.cpp:441-465): the block's cached pixel, else the trace */
+        auto calc = [&](ABlock &b, int x, int y) {
+            if (b.traced(x, y))
+                return b.buf[b.at(x, y)];
+            AV c = traced.at((int64_t)y * gw + x);
+            b.set_traced(x, y, c);
+            return c;
+        };
+        for (ABlock &b : blocks) {
+            want(b.x0, b.y0), want(b.x0 + S, b.y0), want(b.x0, b.y0 + S), want(b.x0 + S, b.y0 + S);
+        }
+        flush();
+        std::vector<ASquare> cur;
+        for (size_t i = 0; i < blocks.size(); i++) { /* RenderBlock::run, :501-507 */
+            ABlock &b = blocks[i];
+            AV tl = calc(b, b.x0, b.y0), tr = calc(b, b.x0 + S, b.y0), bl = calc(b, b.x0, b.y0 + S),
+               br = calc(b, b.x0 + S, b.y0 + S);
+            cur.push_back({(int)i, b.x0, b.y0, S, tl, tr, bl, br});
+        }
+        const float mcd2 = mcd * mcd;
+        auto close = [&](AV a, AV c) { return av_abs2(av_sub(a, c)) <= mcd2 * av_abs2(a); };
+        while (!cur.empty()) { /* renderSquare, :466-499 */
+            std::vector<ASquare> split;
+            for (const ASquare &q : cur) {
+                ABlock &b = blocks[q.b];
+                if (q.x > W || q.y > H)
+                    continue;
+                if (q.size <= 1) {
+                    b.set_traced(q.x, q.y, q.tl);
+                    continue;
+                }
+                if (close(q.tl, q.tr) && close(q.tl, q.bl) && close(q.tl, q.br) && close(q.tr, q.bl) &&
+                    close(q.tr, q.br) && close(q.bl, q.br) && q.size <= maxS) {
+                    for (int yy = 0; yy < q.size; yy++) { /* interpolateSquare, :423-436 */
+                        const float fy = (float)yy / q.size;
+                        const AV l = av_add(q.tl, av_scale(fy, av_sub(q.bl, q.tl)));
+                        const AV r = av_add(q.tr, av_scale(fy, av_sub(q.br, q.tr)));
+                        for (int xx = 0; xx < q.size; xx++) {
+                            const float fx = (float)xx / q.size;
+                            b.set_interp(xx + q.x, yy + q.y, av_add(l, av_scale(fx, av_sub(r, l))));
+                        }
+                    }
+                    continue;
+                }
+                const int h = q.size / 2, cx = q.x + h, cy = q.y + h;
+                auto maybe = [&](int x, int y) {
+                    if (!b.traced(x, y))
+                        want(x, y);
+                };
+                maybe(cx, q.y), maybe(q.x, cy), maybe(cx, cy), maybe(q.x + q.size, cy), maybe(cx, q.y + q.size);
+                split.push_back(q);
+            }
+            flush();
+            std::vector<ASquare> next;
+            for (const ASquare &q : split) {
+                ABlock &b = blocks[q.b];
+                const int h = q.size / 2, cx = q.x + h, cy = q.y + h;
+                const AV tc = calc(b, cx, q.y), cl = calc(b, q.x, cy), cc = calc(b, cx, cy),
+                         cr = calc(b, q.x + q.size, cy), bc = calc(b, cx, q.y + q.size);
+                next.push_back({q.b, q.x, q.y, h, q.tl, tc, cl, cc});
+                next.push_back({q.b, cx, q.y, h, tc, q.tr, cc, cr});
+                next.push_back({q.b, q.x, cy, h, cl, cc, q.bl, bc});
+                next.push_back({q.b, cx, cy, h, cc, cr, bc, q.br});
+            }
+            cur.swap(next);
+        }
+        /* copyToBuffer, :362-374: each block's interior, valid pixels only */
+        std::fill(rgb_out, rgb_out + (size_t)W * H * 3, 0.0f);
+        for (const ABlock &b : blocks)
+            for (int y = b.y0; y < b.y0 + S && y < H; y++)
+                for (int x = b.x0; x < b.x0 + S && x < W; x++)
+                    if (b.st[b.at(x, y)]) {
+                        const AV c = b.buf[b.at(x, y)];
+                        float *o = rgb_out + 3 * ((size_t)y * W + x);
+                        o[0] = c.x, o[1] = c.y, o[2] = c.z;
+                    }
+        if (stats)
+            *stats = acc;
         return PT_OK;
     });
 }

@@ -122,7 +122,7 @@ class DeviceScene:
 
 
 def make_params(width, height, spp, depth, screen=None, seed=0x5EED, order="fast", device=0, pixels=None,
-                max_buffer_bytes=0):
+                max_buffer_bytes=0, grid_width=0):
     sw, sh, dist = screen if screen is not None else (float(width), float(height), float(2 * min(width, height)))
     p = RenderParams()
     p.width, p.height, p.spp, p.depth = int(width), int(height), int(spp), int(depth)
@@ -139,6 +139,7 @@ def make_params(width, height, spp, depth, screen=None, seed=0x5EED, order="fast
         p.pixels = None
         p.npixels = 0
     p.max_buffer_bytes = int(max_buffer_bytes)
+    p.grid_width = int(grid_width)
     return p, keep
 
 
@@ -155,6 +156,25 @@ def render(scene, width: int, height: int, spp: int, depth: int, screen=None, se
     if keep is None:
         out = out.reshape(height, width, 3)
     return (out, st.as_dict()) if stats else out
+
+
+def render_adaptive(scene, width: int, height: int, spp: int, depth: int, screen=None, seed: int = 0x5EED,
+                    order="fast", block_size: int = 0, max_interp: int = 0, min_delta: float = 0.0, device: int = 0):
+    """The reference demo's adaptive image formation (RenderBlock::renderSquare,
+    src/test.cpp:423-507) on the GPU: returns (H x W x 3 image, info dict with
+    traced_pixels, levels and the render stats).  0 selects the demo's block
+    size / interpolation limit / colour threshold."""
+    ds = scene if isinstance(scene, DeviceScene) else DeviceScene(scene)
+    p, _ = make_params(width, height, spp, depth, screen, seed, order, device)
+    ap = _lib.AdaptiveParams()
+    ap.block_size, ap.max_interp, ap.min_delta = int(block_size), int(max_interp), float(min_delta)
+    out = np.zeros((height, width, 3), dtype=np.float32)
+    st = RenderStats()
+    _lib.check(_lib.lib().pt_render_adaptive(ds.handle, ctypes.byref(p), ctypes.byref(ap), out.ctypes.data,
+                                             ctypes.byref(st)))
+    info = st.as_dict()
+    info.update(traced_pixels=int(ap.traced_pixels), levels=int(ap.levels))
+    return out, info
 
 
 def prepare(scene: DeviceScene, params: RenderParams) -> None:

@@ -26,7 +26,12 @@ class RenderParams(ctypes.Structure):
                 ("screen_w", ctypes.c_float), ("screen_h", ctypes.c_float), ("screen_dist", ctypes.c_float),
                 ("seed", ctypes.c_uint64), ("order", ctypes.c_int), ("device", ctypes.c_int),
                 ("pixels", ctypes.POINTER(ctypes.c_int32)), ("npixels", ctypes.c_int64),
-                ("max_buffer_bytes", ctypes.c_int64)]
+                ("max_buffer_bytes", ctypes.c_int64), ("grid_width", ctypes.c_int)]
+
+
+class AdaptiveParams(ctypes.Structure):
+    _fields_ = [("block_size", ctypes.c_int), ("max_interp", ctypes.c_int), ("min_delta", ctypes.c_float),
+                ("traced_pixels", ctypes.c_int64), ("levels", ctypes.c_int)]
 
 
 class RenderStats(ctypes.Structure):
@@ -77,6 +82,8 @@ SIGNATURES = {
     "pt_matrix_concat": (None, [_FP, _FP, _FP]),
     "pt_render": (_I, [_P, ctypes.POINTER(RenderParams), _P, ctypes.POINTER(RenderStats)]),
     "pt_render_device": (_I, [_P, ctypes.POINTER(RenderParams), _P, _P, ctypes.POINTER(RenderStats)]),
+    "pt_render_adaptive": (_I, [_P, ctypes.POINTER(RenderParams), ctypes.POINTER(AdaptiveParams), _P,
+                                ctypes.POINTER(RenderStats)]),
     "pt_prepare": (_I, [_P, ctypes.POINTER(RenderParams)]),
     "pt_scene_compile": (_I, [_P, _I]),
     "pt_scene_kernel_key": (ctypes.c_char_p, [_P, _I]),
