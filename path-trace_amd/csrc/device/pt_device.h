@@ -61,9 +61,9 @@ struct PtLaunch
     int depth;
     int nsamp;          /* samples per pixel slot in this pass                     */
     int s0;             /* first sample index of this pass                         */
-    int gw;             /* pixel index = py * gw + px (gw = W, or W + 1 for the
+    int gw;             /* pixel index = py * gw + px (gw = W, or wider for the
                            adaptive caller's block-edge pixels)                   */
-    int pad1;
+    int chunk;          /* items per work-queue dequeue, 1..64 (0 = PT_CHUNK)      */
 };
 
 struct Env
@@ -1543,7 +1543,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
 #define PT_WPW 4 /* independent waves per workgroup */
 #endif
 #ifndef PT_CHUNK
-#define PT_CHUNK 16 /* (pixel, sample) items a wave takes per dequeue (<= 64) */
+#define PT_CHUNK 16 /* default (pixel, sample) items a wave takes per dequeue (<= 64) */
 #endif
 
 /* The megakernel body.  Persistent: the grid is sized to the resident
@@ -1568,7 +1568,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     Counters &cnt = cbuf[wave];
     cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = cnt.slow = 0;
     const WaveLds L = {qbuf[wave], rbuf[wave], sbuf[wave]};
-    const long long n_chunks = (lp.n_items + PT_CHUNK - 1) / PT_CHUNK;
+    const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
+    const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
     for (;;) {
         long long chunk = 0;
@@ -1577,9 +1578,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         chunk = ((long long)uni((int)(chunk >> 32)) << 32) | (long long)(u32)uni((int)chunk);
         if (chunk >= n_chunks)
             break;
-        const long long item0 = chunk * PT_CHUNK;
+        const long long item0 = chunk * CH;
         V3 mine = mk(0, 0, 0);
-        for (int j = 0; j < PT_CHUNK; j++) {
+        for (int j = 0; j < CH; j++) {
             const long long item = item0 + j;
             if (item >= lp.n_items)
                 break;
@@ -1592,7 +1593,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                 mine = c;
         }
         const long long my = item0 + lane;
-        if (lane < PT_CHUNK && my < lp.n_items) {
+        if (lane < CH && my < lp.n_items) {
             out[3 * my + 0] = mine.x;
             out[3 * my + 1] = mine.y;
             out[3 * my + 2] = mine.z;

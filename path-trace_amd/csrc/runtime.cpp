@@ -65,7 +65,7 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     int depth;
     int nsamp;
     int s0;
-    int gw, pad1;
+    int gw, chunk;
 };
 
 template <class T>
@@ -560,7 +560,13 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
     for (int s0 = 0; s0 < p->spp; s0 += (int)per_pass) {
         int nsamp = (int)std::min<long long>(per_pass, p->spp - s0);
         long long n_items = npix * nsamp;
-        long long chunks = (n_items + 15) / 16;
+        /* 16 items per dequeue amortise the queue; a launch too small to give
+         * every resident wave a few chunks takes fewer, so one wave does not
+         * trace many samples of one expensive pixel while others idle */
+        const long long waves = (long long)ds.resident_blocks * ds.wpw;
+        int chunk = 16;
+        while (chunk > 1 && n_items / chunk < 4 * waves) chunk /= 2;
+        long long chunks = (n_items + chunk - 1) / chunk;
         const int wpw = ds.wpw;
         {
             long long blocks = std::min<long long>(ds.resident_blocks, (chunks + wpw - 1) / wpw);
@@ -576,6 +582,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             lp.nsamp = nsamp;
             lp.s0 = s0;
             lp.gw = p->grid_width > 0 ? p->grid_width : p->width;
+            lp.chunk = chunk;
             const float *Pp = ds.P.p;
             const PtImageDev *ip = ds.imgs.p;
             const uint64_t *jp = ds.jump.p;

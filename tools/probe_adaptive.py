@@ -1,0 +1,26 @@
+"""Adaptive caller (pt_render_adaptive) on a full benchmark frame vs the plain
+full-frame render at the same spp.  usage: probe_adaptive.py CONFIG SPP"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "path-trace_amd"))
+import numpy as np  # noqa: E402
+import pathtrace as pt  # noqa: E402
+from pathtrace import scenes  # noqa: E402
+
+name, spp = sys.argv[1], int(sys.argv[2])
+cfg = scenes.CONFIGS[name]
+ds = pt.DeviceScene(cfg.scene())
+t = time.time()
+img, info = pt.render_adaptive(ds, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen)
+ta = time.time() - t
+t = time.time()
+full, st = pt.render(ds, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
+tf = time.time() - t
+rmse = np.sqrt(np.mean((img.astype(np.float64) - full) ** 2, axis=(0, 1))).tolist()
+print(json.dumps({"config": name, "spp": spp, "adaptive_wall_s": ta, "adaptive_kernel_ms": info["kernel_ms"],
+                  "traced_pixels": info["traced_pixels"], "traced_frac": info["traced_pixels"] / (cfg.width * cfg.height),
+                  "levels": info["levels"], "full_wall_s": tf, "full_kernel_ms": st["kernel_ms"],
+                  "rmse_adaptive_vs_full": rmse}), flush=True)
