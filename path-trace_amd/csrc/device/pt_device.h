@@ -288,13 +288,10 @@ __device__ __forceinline__ u32 rng_next(Rng &r)
 }
 /* uniform_real_distribution<float>, vector3d.h:22-33, for (0,1) and (-1,1) */
 __device__ __forceinline__ float u01(u32 o) { return (float)o / 4294967296.0f; }
-__device__ __forceinline__ float u11(u32 o)
-{
-    float r = (float)o / 4294967296.0f;
-    r *= 2.0f;
-    r += -1.0f;
-    return r;
-}
+/* uniform(-1, 1): (float)o / 2^32 * (1 - -1) + -1 (include/vector3d.h:14-34).
+ * Both power-of-two scalings are exact for o >= 1 (and 0 stays 0), so one
+ * multiply by 2^-31 gives the same bits. */
+__device__ __forceinline__ float u11(u32 o) { return (float)o * 0x1p-31f + -1.0f; }
 
 /* --------------------------------------------------------- wave helpers --- */
 __device__ __forceinline__ float rdlane(float v, int l)
@@ -1062,7 +1059,7 @@ struct Attempt
 
 /* The predicates are balloted where they are produced, so they never pass
  * through a per-lane integer. */
-template <bool DEFERRED>
+template <bool DEFERRED, bool KR0>
 __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float sc, float sNa, float abs_rc,
                                            bool child_leaf_depth)
 {
@@ -1072,7 +1069,9 @@ __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float s
     /* rand(): while (mag > max) with mag = sqrt(|v|^2); correctly rounded
      * sqrt(x) > 1  <=>  x > 1 + 2^-23 (exhaustively checked) */
     const bool ball = !(dot(v, v) > 0x1.000002p+0f);
-    const V3 w = v + kR;
+    /* KR0: scatter coefficient 1 makes kR = 0 * reflectedRayDir = +-0 per
+     * component, and v + +-0 == v because u11 never yields -0 */
+    const V3 w = KR0 ? v : v + kR;
     const bool hemi = !(dot(n, w) <= EPS); /* while (dot(normal, dir) <= eps) */
     Attempt a;
     a.A = __ballot(ball && hemi);
@@ -1161,7 +1160,7 @@ __device__ __forceinline__ int replay(u64 A, u64 F, u64 NL, int rem, int &fails,
  * count > 1000 early return (path-trace.h:149-152), B_NONLEAF after writing
  * the next child's ray into `child` when that child must recurse (it draws
  * random numbers, so it runs on the spine). */
-template <class S, bool STRICT, bool DEFERRED>
+template <class S, bool STRICT, bool DEFERRED, bool KR0>
 __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
@@ -1197,7 +1196,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 for (int k = 0; k < PT_KATT; k++) {
                     if (k)
                         sk = A64 * sk + g64inc;
-                    at[k] = attempt<DEFERRED>(sk, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
+                    at[k] = attempt<DEFERRED, KR0>(sk, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
                     Am[k] = at[k].A;
                     Fm[k] = at[k].F;
                     NLm[k] = at[k].NL;
@@ -1385,9 +1384,12 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
     const float sNa = unif((unif(f.strength) / (float)uni(f.N)) * unif(f.add));
     const float abs_rc = unif(length(univ(f.rc)));
     const bool deferred = uni(f.depth) - 1 <= 0 || (sNa * abs_rc * 1.01f < EPS);
-    if (deferred)
-        return burst_t<S, STRICT, true>(e, rng, jump, A3l, G3l, L, f, child, cnt);
-    return burst_t<S, STRICT, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+    if (deferred) {
+        if (unif(f.sc) == 1.0f)
+            return burst_t<S, STRICT, true, true>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+        return burst_t<S, STRICT, true, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+    }
+    return burst_t<S, STRICT, false, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
 }
 
 enum { PH_ENTER, PH_SETUP, PH_LOOP, PH_RETURN };
