@@ -132,6 +132,7 @@ typedef struct pt_render_stats {
     uint64_t rounds;               /* attempt rounds                                            */
     uint64_t sphere_tests, sphere_hits, plane_tests;
     uint64_t slow_queries;         /* leaf children that needed the full CSG merge (slow pass)  */
+    uint64_t dark_queries;         /* leaf children no emissive primitive can light: weight * 0 */
 } pt_render_stats;
 
 /* Synchronous: renders the frame into rgb_out (host memory), which receives,

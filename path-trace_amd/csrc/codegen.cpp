@@ -228,6 +228,20 @@ Generated generate(const SceneImpl &s, int depth)
             src << "    case " << k << ": return " << mt[k].*field << "::" << fn << "(p, e);\n";
         src << "    default: return " << (std::string(ret) == "V3" ? "mk(0, 0, 0)" : "0.0f") << ";\n    }\n  }\n";
     };
+    /* dark(m): material m's emission is the constant (+0, +0, +0), so a leaf
+     * child whose first hit is m (or a miss) contributes weight * +0 */
+    src << "  __device__ static constexpr bool dark(int m) { return ";
+    for (size_t k = 0; k < g.mats.size(); k++) {
+        const TexRec &e = s.textures.at(s.materials.at(g.mats[k]).emissive);
+        bool z = e.kind == TexKind::Color;
+        for (int c = 0; c < 3 && z; c++) {
+            uint32_t bits;
+            memcpy(&bits, &e.f[c], 4);
+            z = bits == 0u;
+        }
+        src << "m == " << k << " ? " << (z ? "true" : "false") << " : ";
+    }
+    src << "false; }\n";
     if (all_emis_const) {
         src << "  __device__ static __forceinline__ V3 emis(int m, V3, const Env &e) {\n"
             << "    const float *t = e.P + " << emis_tab << " + 3 * m;\n    return mk(t[0], t[1], t[2]);\n  }\n";

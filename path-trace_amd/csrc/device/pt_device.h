@@ -455,6 +455,19 @@ struct Sph
     }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { f(IC<PRIM>(), IC<MAT>()); }
+    /* the same for primitives whose material SEL selects, all primitives not just positive ones */
+    template <class SEL, class PS>
+    __device__ static __forceinline__ void span_sel(PS &ps, const Ctx &c, const Ray &q, const Env &e)
+    {
+        if constexpr (SEL::take(MAT))
+            span(ps, c, q, e);
+    }
+    template <class SEL, class F>
+    __device__ static __forceinline__ void each_sel(F &&f)
+    {
+        if constexpr (SEL::take(MAT))
+            f(IC<PRIM>());
+    }
     template <class PS>
     __device__ static __forceinline__ int fast_ok(const PS &) { return 1; }
     __device__ static __forceinline__ V3 normal(int, float t, V3 o, V3 d, const Env &e)
@@ -515,6 +528,19 @@ struct Pln
     }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { f(IC<PRIM>(), IC<MAT>()); }
+    /* the same for primitives whose material SEL selects, all primitives not just positive ones */
+    template <class SEL, class PS>
+    __device__ static __forceinline__ void span_sel(PS &ps, const Ctx &c, const Ray &q, const Env &e)
+    {
+        if constexpr (SEL::take(MAT))
+            span(ps, c, q, e);
+    }
+    template <class SEL, class F>
+    __device__ static __forceinline__ void each_sel(F &&f)
+    {
+        if constexpr (SEL::take(MAT))
+            f(IC<PRIM>());
+    }
     template <class PS>
     __device__ static __forceinline__ int fast_ok(const PS &) { return 1; }
     __device__ static __forceinline__ V3 normal(int, float, V3, V3, const Env &e)
@@ -557,6 +583,18 @@ struct Pln
     {                                                                                               \
         A::span(ps, c.a, q, e);                                                                     \
         B::span(ps, c.b, q, e);                                                                     \
+    }                                                                                               \
+    template <class SEL, class PS>                                                                  \
+    __device__ static __forceinline__ void span_sel(PS &ps, const Ctx &c, const Ray &q, const Env &e) \
+    {                                                                                               \
+        A::template span_sel<SEL>(ps, c.a, q, e);                                                   \
+        B::template span_sel<SEL>(ps, c.b, q, e);                                                   \
+    }                                                                                               \
+    template <class SEL, class F>                                                                   \
+    __device__ static __forceinline__ void each_sel(F &&f)                                          \
+    {                                                                                               \
+        A::template each_sel<SEL>(f);                                                               \
+        B::template each_sel<SEL>(f);                                                               \
     }                                                                                               \
     template <class PS>                                                                             \
     __device__ static __forceinline__ int fast_ok(const PS &ps)                                     \
@@ -730,6 +768,13 @@ struct Xf
     }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { C::each_pos(f); }
+    template <class SEL, class PS>
+    __device__ static __forceinline__ void span_sel(PS &ps, const Ctx &c, const Ray &q, const Env &e)
+    {
+        C::template span_sel<SEL>(ps, c.c, mkray(m_lin(e.P + MOFF, q.d)), e);
+    }
+    template <class SEL, class F>
+    __device__ static __forceinline__ void each_sel(F &&f) { C::template each_sel<SEL>(f); }
     template <class PS>
     __device__ static __forceinline__ int fast_ok(const PS &ps) { return C::fast_ok(ps); }
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)
@@ -791,6 +836,13 @@ __device__ __forceinline__ bool fast_first_hit(const PS &ps, float &t, int &mat)
     t = b1;
     return true;
 }
+
+/* Selects the primitives whose material may emit (scene S::dark is false). */
+template <class S>
+struct Emissive
+{
+    __device__ static constexpr bool take(int m) { return !S::dark(m); }
+};
 
 /* ------------------------------------------------------------ textures --- */
 __device__ __forceinline__ float mean3(V3 c) { return ((c.x + c.y) + c.z) * (1.0f / 3.0f); } /* texture.h:14-18 */
@@ -1005,15 +1057,16 @@ struct TSpherical
 /* Per-wave statistics, kept in LDS (every lane writes the same value). */
 struct Counters
 {
-    u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow;
+    u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow, dark;
 };
 
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
-    float4 *q;    /* PT_QCAP queued leaf-child rays (direction, factor)        */
-    float4 *ring; /* PT_RCAP child slots: parked ray, then the child's term   */
-    int *slowq;   /* PT_SCAP slot positions waiting for the full merge        */
+    float4 *q;            /* PT_QCAP queued leaf-child rays (direction, factor)           */
+    float4 *ring;         /* PT_RCAP child slots: parked ray, then the child's term      */
+    unsigned char *fastq; /* PT_SCAP slots waiting for the fast pass (position mod 256) */
+    unsigned char *slowq; /* PT_SCAP slots waiting for the full merge                   */
 };
 
 /* ---------------------------------------------------------------- spine --- */
@@ -1044,7 +1097,7 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #endif
 #define PT_QCAP 256 /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
 #define PT_RCAP 256 /* child slots per wave awaiting their group sum               */
-#define PT_SCAP 128 /* parked children per wave: < 64 + one fast pass               */
+#define PT_SCAP 256 /* parked children per queue (byte offsets): a drain can add 2 x 64 to < 64 */
 static_assert(64 + 64 * PT_KATT <= PT_QCAP, "queue too small for PT_KATT");
 #define PT_JUMP_ENTRIES 193 /* host table: m = 0..192 attempts (PT_KATT <= 3) */
 
@@ -1165,7 +1218,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
     float4 *const q = L.q, *const ring = L.ring;
-    int *const slowq = L.slowq;
+    unsigned char *const fastq = L.fastq, *const slowq = L.slowq;
     const int lane = threadIdx.x & 63;
     const u64 below = (1ull << lane) - 1ull;
     const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
@@ -1182,9 +1235,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const u64 A64 = jump[128], g64inc = jump[129] * rng.inc;   /* 64 attempts = 192 draws  */
     const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * rng.inc; /* a full round */
     int qhead = 0, qn = 0, fails = 0, reason = -1;
-    int npos = 0, sum_ptr = 0, s_head = 0, s_n = 0; /* slot ring / slow queue positions */
+    int npos = 0, sum_ptr = 0, f_head = 0, f_n = 0, s_head = 0, s_n = 0; /* slot ring / queue positions */
     int fast_on = 1;
-    u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0;
+    u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
     for (;;) {
         if (reason < 0 && qn < 64) {
             /* ---- generation round: lane l evaluates attempts l, 64 + l, ... */
@@ -1250,11 +1303,14 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
         }
         if (qn >= 64 || (reason >= 0 && qn > 0)) {
-            /* ---- fast pass: one queued leaf child per lane.  Lanes whose spans
-             * pass the fast check finish here and leave their term in the slot
-             * ring; the others leave their ray there and queue for a slow pass. */
+            /* ---- stage A: one queued leaf child per lane.  A child whose ray no
+             * emissive primitive meets at t >= eps has the term weight * (+0)
+             * whatever the CSG makes of it (merges only copy primitive
+             * boundaries, and the scan qualifies a boundary only at t >= eps):
+             * it finishes here.  The others park their ray in the slot ring and
+             * queue for the fast pass. */
             const int cntb = qn < 64 ? qn : 64;
-            int slow = 0;
+            int lit = 0;
             if (lane < cntb) {
                 float4 en = q[(qhead + lane) & (PT_QCAP - 1)];
                 V3 dir = mk(en.x, en.y, en.z);
@@ -1263,11 +1319,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
                 }
                 float4 out;
-                if (!fast_on) {
-                    /* the fast check keeps failing in this burst: park every child */
-                    slow = 1;
-                    out = make_float4(dir.x, dir.y, dir.z, en.w);
-                } else {
 #if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
                 /* experiment: generation cost only */
                 {
@@ -1276,6 +1327,54 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     out = make_float4(term.x, term.y, term.z, 0.0f);
                 }
 #else
+                {
+                    typename S::Root::Ctx ctx;
+                    S::Root::prep(ctx, hit, e);
+                    PrimSpans<S::Root::HI> ps;
+                    S::Root::template span_sel<Emissive<S>>(ps, ctx, mkray(dir), e);
+                    S::Root::template each_sel<Emissive<S>>([&](auto x) {
+                        constexpr int X = decltype(x)::value;
+                        lit |= ps.live[X] & (ps.t1[X] >= EPS);
+                    });
+                }
+                if (lit) {
+                    out = make_float4(dir.x, dir.y, dir.z, en.w);
+                } else {
+                    const V3 term = ((aN * en.w) * rc) * mk(0.0f, 0.0f, 0.0f);
+                    out = make_float4(term.x, term.y, term.z, 0.0f);
+                }
+#endif
+                ring[(npos + lane) & (PT_RCAP - 1)] = out;
+            }
+            const u64 LM = __ballot(lit);
+            if (lit)
+                fastq[(f_head + f_n + __popcll(LM & below)) & (PT_SCAP - 1)] = (unsigned char)(npos + lane);
+            f_n += __popcll(LM);
+            n_dark += (u32)(cntb - __popcll(LM));
+            npos += cntb;
+            n_leaf += (u32)cntb;
+            qhead += cntb;
+            qn -= cntb;
+            i += cntb;
+        }
+        const bool final = reason >= 0 && qn == 0;
+        /* queued slots hold positions mod 256; every pending position lies in
+         * [sum_ptr, sum_ptr + PT_RCAP), which restores it */
+        auto slot_pos = [&](unsigned char v) { return sum_ptr + ((int)(v - sum_ptr) & (PT_RCAP - 1)); };
+        const bool pressure = npos - sum_ptr > PT_RCAP - 64;
+        /* ---- stage B: fast pass over 64 parked children.  Lanes whose spans
+         * pass the fast check finish; the others stay parked for the full merge */
+        while (f_n > 0 && (f_n >= 64 || final || pressure)) {
+            const int cf = f_n < 64 ? f_n : 64;
+            int slow = 0, pos = 0;
+            if (lane < cf && !fast_on) {
+                /* the fast check keeps failing in this burst: park for the full merge */
+                pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
+                slow = 1;
+            } else if (lane < cf) {
+                pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
+                const float4 en = ring[pos & (PT_RCAP - 1)];
+                const V3 dir = mk(en.x, en.y, en.z);
                 typename S::Root::Ctx ctx;
                 S::Root::prep(ctx, hit, e);
                 PrimSpans<S::Root::HI> ps;
@@ -1287,42 +1386,33 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     if (fast_first_hit<typename S::Root>(ps, t, mat))
                         col = S::emis(mat, hit + t * dir, e);
                     const V3 term = ((aN * en.w) * rc) * col;
-                    out = make_float4(term.x, term.y, term.z, 0.0f);
+                    ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
                 } else {
 #if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 3
-                    /* experiment: fast pass only (slow lanes contribute 0) */
-                    out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    /* experiment: no slow passes (slow lanes contribute 0) */
+                    ring[pos & (PT_RCAP - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #else
                     slow = 1;
-                    out = make_float4(dir.x, dir.y, dir.z, en.w);
 #endif
                 }
-#endif
-                }
-                ring[(npos + lane) & (PT_RCAP - 1)] = out;
             }
             const u64 SM = __ballot(slow);
-            /* scenes whose spans overlap almost everywhere (e.g. a box of sky
-             * half-spaces) skip the fast pass for the rest of the burst */
-            if (fast_on && 4 * __popcll(SM) > 3 * cntb)
-                fast_on = 0;
             if (slow)
-                slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = npos + lane;
+                slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = (unsigned char)pos;
             s_n += __popcll(SM);
-            npos += cntb;
-            n_leaf += (u32)cntb;
             n_slow += (u32)__popcll(SM);
-            qhead += cntb;
-            qn -= cntb;
-            i += cntb;
+            /* overlap-heavy scenes (e.g. a box of sky half-spaces) stop trying */
+            if (fast_on && 4 * __popcll(SM) > 3 * cf)
+                fast_on = 0;
+            f_head += cf;
+            f_n -= cf;
         }
-        const bool final = reason >= 0 && qn == 0;
-        /* ---- slow passes: 64 parked children at a time through the full merge,
-         * when 64 are waiting, the slot ring is filling up, or at the end */
-        while (s_n > 0 && (s_n >= 64 || final || npos - sum_ptr > PT_RCAP - 64)) {
+        /* ---- stage C: slow passes, 64 parked children at a time through the
+         * full merge */
+        while (s_n > 0 && (s_n >= 64 || final || pressure)) {
             const int cs = s_n < 64 ? s_n : 64;
             if (lane < cs) {
-                const int pos = slowq[(s_head + lane) & (PT_SCAP - 1)];
+                const int pos = slot_pos(slowq[(s_head + lane) & (PT_SCAP - 1)]);
                 const float4 en = ring[pos & (PT_RCAP - 1)];
                 const V3 dir = mk(en.x, en.y, en.z);
                 typename S::Root::Ctx ctx;
@@ -1342,8 +1432,12 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
         /* ---- sum finished groups in order: 64 children per group (the last
          * group of a burst may be shorter), group-64 tree or sequential */
         {
-            const int resolved = s_n ? uni(slowq[s_head & (PT_SCAP - 1)]) : npos;
-            while (sum_ptr < resolved && (resolved - sum_ptr >= 64 || (final && s_n == 0))) {
+            int resolved = npos;
+            if (s_n)
+                resolved = slot_pos(uni(slowq[s_head & (PT_SCAP - 1)]));
+            if (f_n)
+                resolved = min(resolved, slot_pos(uni(fastq[f_head & (PT_SCAP - 1)])));
+            while (sum_ptr < resolved && (resolved - sum_ptr >= 64 || (final && s_n == 0 && f_n == 0))) {
                 const int cg = (npos - sum_ptr) < 64 ? (npos - sum_ptr) : 64;
                 V3 term = mk(-0.0f, -0.0f, -0.0f);
                 if (lane < cg) {
@@ -1369,6 +1463,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     cnt.attempts += n_att;
     cnt.leaf += n_leaf;
     cnt.slow += n_slow;
+    cnt.dark += n_dark;
     return reason;
 }
 
@@ -1562,14 +1657,15 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     __shared__ Frame stk[PT_WPW][MAXD + 1];
     __shared__ float4 qbuf[PT_WPW][PT_QCAP];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
-    __shared__ int sbuf[PT_WPW][PT_SCAP];
+    __shared__ unsigned char fbuf[PT_WPW][PT_SCAP];
+    __shared__ unsigned char sbuf[PT_WPW][PT_SCAP];
     __shared__ Counters cbuf[PT_WPW];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const Env e = {P, imgs};
     const u64 A3l = jump[2 * lane], G3l = jump[2 * lane + 1];
     Counters &cnt = cbuf[wave];
-    cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = cnt.slow = 0;
-    const WaveLds L = {qbuf[wave], rbuf[wave], sbuf[wave]};
+    cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = cnt.slow = cnt.dark = 0;
+    const WaveLds L = {qbuf[wave], rbuf[wave], fbuf[wave], sbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
@@ -1609,6 +1705,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         atomicAdd(&stats[4], cnt.shaded);
         atomicAdd(&stats[5], cnt.nonleaf);
         atomicAdd(&stats[6], cnt.slow);
+        atomicAdd(&stats[7], cnt.dark);
     }
 }
 

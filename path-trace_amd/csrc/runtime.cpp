@@ -642,6 +642,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
         st->attempts = c[2];
         st->rounds = c[3];
         st->slow_queries = c[6];
+        st->dark_queries = c[7];
         st->sphere_tests = st->queries * (uint64_t)g.n_spheres;
         st->plane_tests = st->queries * (uint64_t)g.n_planes;
         for (auto e : evs) (void)hipEventDestroy(e);
@@ -1094,6 +1095,7 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
             acc.kernel_ms += st.kernel_ms, acc.reduce_ms += st.reduce_ms, acc.launches += st.launches;
             acc.samples += st.samples, acc.queries += st.queries, acc.leaf_queries += st.leaf_queries;
             acc.attempts += st.attempts, acc.rounds += st.rounds, acc.slow_queries += st.slow_queries;
+            acc.dark_queries += st.dark_queries;
             ap->traced_pixels += (int64_t)need.size();
             ap->levels++;
             need.clear();
