@@ -1058,7 +1058,22 @@ struct TSpherical
 struct Counters
 {
     u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow, dark;
+#ifdef PT_PHASE_TIMING
+    u64 ph[7]; /* cycles: generation, stage A, fast pass, slow pass, group sums, burst total, sample total */
+    u64 np[8]; /* events: bursts, loop iterations, stage-A passes, fast passes, slow passes, group sums, fast lanes, slow lanes */
+#define PT_CNT(c, k, v) (c).np[k] += (v)
+#else
+#define PT_CNT(c, k, v)
+#endif
 };
+/* Per-phase wave cycle counters (profiling builds only: PT_DEVICE_DEFINES="PT_PHASE_TIMING") */
+#ifdef PT_PHASE_TIMING
+#define PT_T0(v) const u64 v = __builtin_amdgcn_s_memtime()
+#define PT_ACC(c, k, v) (c).ph[k] += __builtin_amdgcn_s_memtime() - (v)
+#else
+#define PT_T0(v)
+#define PT_ACC(c, k, v)
+#endif
 
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
@@ -1238,8 +1253,11 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     int npos = 0, sum_ptr = 0, f_head = 0, f_n = 0, s_head = 0, s_n = 0; /* slot ring / queue positions */
     int fast_on = 1;
     u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
+    PT_CNT(cnt, 0, 1);
     for (;;) {
+        PT_CNT(cnt, 1, 1);
         if (reason < 0 && qn < 64) {
+            PT_T0(tg);
             /* ---- generation round: lane l evaluates attempts l, 64 + l, ... */
             Attempt at[PT_KATT];
             u64 Am[PT_KATT], Fm[PT_KATT], NLm[PT_KATT];
@@ -1301,8 +1319,10 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 rng.st = Afull * rng.st + gfullinc;
             else
                 rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
+            PT_ACC(cnt, 0, tg);
         }
         if (qn >= 64 || (reason >= 0 && qn > 0)) {
+            PT_T0(ta);
             /* ---- stage A: one queued leaf child per lane.  A child whose ray no
              * emissive primitive meets at t >= eps has the term weight * (+0)
              * whatever the CSG makes of it (merges only copy primitive
@@ -1310,6 +1330,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
              * it finishes here.  The others park their ray in the slot ring and
              * queue for the fast pass. */
             const int cntb = qn < 64 ? qn : 64;
+            PT_CNT(cnt, 2, 1);
             int lit = 0;
             if (lane < cntb) {
                 float4 en = q[(qhead + lane) & (PT_QCAP - 1)];
@@ -1356,16 +1377,20 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             qhead += cntb;
             qn -= cntb;
             i += cntb;
+            PT_ACC(cnt, 1, ta);
         }
         const bool final = reason >= 0 && qn == 0;
         /* queued slots hold positions mod 256; every pending position lies in
          * [sum_ptr, sum_ptr + PT_RCAP), which restores it */
         auto slot_pos = [&](unsigned char v) { return sum_ptr + ((int)(v - sum_ptr) & (PT_RCAP - 1)); };
         const bool pressure = npos - sum_ptr > PT_RCAP - 64;
+        PT_T0(tb);
         /* ---- stage B: fast pass over 64 parked children.  Lanes whose spans
          * pass the fast check finish; the others stay parked for the full merge */
         while (f_n > 0 && (f_n >= 64 || final || pressure)) {
             const int cf = f_n < 64 ? f_n : 64;
+            PT_CNT(cnt, 3, 1);
+            PT_CNT(cnt, 6, cf);
             int slow = 0, pos = 0;
             if (lane < cf && !fast_on) {
                 /* the fast check keeps failing in this burst: park for the full merge */
@@ -1407,10 +1432,14 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             f_head += cf;
             f_n -= cf;
         }
+        PT_ACC(cnt, 2, tb);
+        PT_T0(tc);
         /* ---- stage C: slow passes, 64 parked children at a time through the
          * full merge */
         while (s_n > 0 && (s_n >= 64 || final || pressure)) {
             const int cs = s_n < 64 ? s_n : 64;
+            PT_CNT(cnt, 4, 1);
+            PT_CNT(cnt, 7, cs);
             if (lane < cs) {
                 const int pos = slot_pos(slowq[(s_head + lane) & (PT_SCAP - 1)]);
                 const float4 en = ring[pos & (PT_RCAP - 1)];
@@ -1429,6 +1458,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             s_head += cs;
             s_n -= cs;
         }
+        PT_ACC(cnt, 3, tc);
+        PT_T0(ts);
         /* ---- sum finished groups in order: 64 children per group (the last
          * group of a burst may be shorter), group-64 tree or sequential */
         {
@@ -1439,6 +1470,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 resolved = min(resolved, slot_pos(uni(fastq[f_head & (PT_SCAP - 1)])));
             while (sum_ptr < resolved && (resolved - sum_ptr >= 64 || (final && s_n == 0 && f_n == 0))) {
                 const int cg = (npos - sum_ptr) < 64 ? (npos - sum_ptr) : 64;
+                PT_CNT(cnt, 5, 1);
                 V3 term = mk(-0.0f, -0.0f, -0.0f);
                 if (lane < cg) {
                     const float4 tv = ring[(sum_ptr + lane) & (PT_RCAP - 1)];
@@ -1454,6 +1486,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 sum_ptr += cg;
             }
         }
+        PT_ACC(cnt, 4, ts);
         if (final)
             break;
     }
@@ -1479,12 +1512,18 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
     const float sNa = unif((unif(f.strength) / (float)uni(f.N)) * unif(f.add));
     const float abs_rc = unif(length(univ(f.rc)));
     const bool deferred = uni(f.depth) - 1 <= 0 || (sNa * abs_rc * 1.01f < EPS);
+    PT_T0(t0);
+    int r;
     if (deferred) {
         if (unif(f.sc) == 1.0f)
-            return burst_t<S, STRICT, true, true>(e, rng, jump, A3l, G3l, L, f, child, cnt);
-        return burst_t<S, STRICT, true, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+            r = burst_t<S, STRICT, true, true>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+        else
+            r = burst_t<S, STRICT, true, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+    } else {
+        r = burst_t<S, STRICT, false, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
     }
-    return burst_t<S, STRICT, false, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+    PT_ACC(cnt, 5, t0);
+    return r;
 }
 
 enum { PH_ENTER, PH_SETUP, PH_LOOP, PH_RETURN };
@@ -1665,6 +1704,12 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     const u64 A3l = jump[2 * lane], G3l = jump[2 * lane + 1];
     Counters &cnt = cbuf[wave];
     cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = cnt.slow = cnt.dark = 0;
+#ifdef PT_PHASE_TIMING
+    for (int k = 0; k < 7; k++)
+        cnt.ph[k] = 0;
+    for (int k = 0; k < 8; k++)
+        cnt.np[k] = 0;
+#endif
     const WaveLds L = {qbuf[wave], rbuf[wave], fbuf[wave], sbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
@@ -1685,8 +1730,10 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             const long long slot = item / lp.nsamp;
             const int s = lp.s0 + (int)(item - slot * lp.nsamp);
             const int pix = pixels ? pixels[slot] : (int)slot;
+            PT_T0(tt);
             V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], L, jump, A3l, G3l,
                                                  cnt);
+            PT_ACC(cnt, 6, tt);
             if (lane == j)
                 mine = c;
         }
@@ -1706,6 +1753,12 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         atomicAdd(&stats[5], cnt.nonleaf);
         atomicAdd(&stats[6], cnt.slow);
         atomicAdd(&stats[7], cnt.dark);
+#ifdef PT_PHASE_TIMING
+        for (int k = 0; k < 7; k++)
+            atomicAdd(&stats[8 + k], cnt.ph[k]);
+        for (int k = 0; k < 8; k++)
+            atomicAdd(&stats[16 + k], cnt.np[k]);
+#endif
     }
 }
 

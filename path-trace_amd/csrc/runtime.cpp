@@ -420,7 +420,7 @@ DeviceState &device_state(SceneImpl &s, int device, const Generated &g)
         std::vector<uint64_t> jt = jump_table();
         ds->jump.ensure(jt.size());
         HIPCHECK(hipMemcpy(ds->jump.p, jt.data(), jt.size() * 8, hipMemcpyHostToDevice));
-        ds->stats.ensure(16);
+        ds->stats.ensure(32);
     }
     if (ds->key != g.key) {
         const std::vector<char> &code = code_object(g);
@@ -546,7 +546,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
     const long long per_pass = pass_samples(p, npix);
     if (st)
         memset(st, 0, sizeof(*st));
-    HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 16 * 8, stream));
+    HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 32 * 8, stream));
     hipFunction_t fn = p->order == PT_ORDER_REFERENCE ? ds.strict : ds.fast;
     std::vector<hipEvent_t> evs;
     auto event = [&]() {
@@ -635,7 +635,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             HIPCHECK(hipEventElapsedTime(&ms, evs[sp.first], evs[sp.second]));
             st->reduce_ms += ms;
         }
-        uint64_t c[16];
+        uint64_t c[32];
         HIPCHECK(hipMemcpy(c, ds.stats.p, sizeof c, hipMemcpyDeviceToHost));
         st->queries = c[0] + c[1];
         st->leaf_queries = c[1];
@@ -643,6 +643,15 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
         st->rounds = c[3];
         st->slow_queries = c[6];
         st->dark_queries = c[7];
+        if (getenv("PT_PHASE_DUMP")) /* profiling builds (PT_PHASE_TIMING): per-phase wave cycles */
+        {
+            fprintf(stderr, "pt_phases");
+            for (int k = 8; k < 15; k++)
+                fprintf(stderr, " %llu", (unsigned long long)c[k]);
+            for (int k = 16; k < 24; k++)
+                fprintf(stderr, " %llu", (unsigned long long)c[k]);
+            fprintf(stderr, "\n");
+        }
         st->sphere_tests = st->queries * (uint64_t)g.n_spheres;
         st->plane_tests = st->queries * (uint64_t)g.n_planes;
         for (auto e : evs) (void)hipEventDestroy(e);

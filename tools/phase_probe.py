@@ -1,0 +1,31 @@
+"""Per-phase wave-cycle split of the C3 render kernel (profiling build).
+Runs tools/perf_probe.py with PT_DEVICE_DEFINES=PT_PHASE_TIMING and
+PT_PHASE_DUMP=1 and prints each phase's share of the sample total.
+usage: phase_probe.py [spp] [extra defines]"""
+import os
+import subprocess
+import sys
+
+here = os.path.dirname(os.path.abspath(__file__))
+spp = sys.argv[1] if len(sys.argv) > 1 else "16"
+defs = " ".join(["PT_PHASE_TIMING"] + sys.argv[2:])
+env = dict(os.environ, PT_DEVICE_DEFINES=defs, PT_PHASE_DUMP="1")
+r = subprocess.run([sys.executable, os.path.join(here, "perf_probe.py"), spp], env=env, capture_output=True,
+                   text=True, timeout=900)
+print(r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "no stdout", r.stderr[-1500:] if r.returncode else "")
+names = ["generation", "stageA", "fastpass", "slowpass", "groupsum", "burst", "sample"]
+for line in r.stderr.splitlines():
+    if line.startswith("pt_phases"):
+        v = [int(x) for x in line.split()[1:]]
+        tot = v[6]
+        for n, x in zip(names, v):
+            print("%-12s %6.1f%%" % (n, 100.0 * x / tot))
+        print("%-12s %6.1f%%" % ("spine", 100.0 * (v[6] - v[5]) / tot))
+        print("%-12s %6.1f%%" % ("burst-other", 100.0 * (v[5] - sum(v[:5])) / tot))
+        if len(v) >= 15:
+            import json as _j
+            smp = _j.loads(r.stdout.strip().splitlines()[-1])["samples"]
+            ev = ["bursts", "iterations", "stageA_passes", "fast_passes", "slow_passes", "group_sums",
+                  "fast_lanes", "slow_lanes"]
+            for n, x in zip(ev, v[7:15]):
+                print("%-14s %10.3f per sample" % (n, x / smp))
