@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <fstream>
 #include <sstream>
 
 #include "internal.h"
@@ -217,7 +218,16 @@ Generated generate(const SceneImpl &s, int depth)
             src << "#define " << (eq == std::string::npos ? d : d.substr(0, eq) + " " + d.substr(eq + 1)) << "\n";
         }
     }
-    src << device_library_source() << "\n";
+    /* experiment hook: A/B a different device library text in the same run,
+     * e.g. PT_DEVICE_HEADER=tools/ab/old.h (profiling only) */
+    if (const char *hdr = getenv("PT_DEVICE_HEADER")) {
+        std::ifstream f(hdr);
+        if (!f)
+            throw Error(PT_ERR_ARG, std::string("PT_DEVICE_HEADER not readable: ") + hdr);
+        src << f.rdbuf() << "\n";
+    } else {
+        src << device_library_source() << "\n";
+    }
     src << "namespace ptgen {\nusing namespace ptd;\n";
     src << "typedef " << root << " RootT;\n";
     src << "struct Scene {\n  typedef RootT Root;\n";

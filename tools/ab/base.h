@@ -1,4 +1,4 @@
-R"PTDEV(/*
+/*
  * pt_device.h -- CDNA4 (gfx950) device library of the MI355X path tracer.
  *
  * Embedded verbatim into every scene module that the runtime generates and
@@ -1079,8 +1079,7 @@ struct Counters
 struct WaveLds
 {
     float4 *q;            /* PT_QCAP queued leaf-child rays (direction, factor)           */
-    float4 *ring;         /* PT_RCAP kept-child slots: parked ray, then the child's term */
-    u64 *gmask;           /* PT_GCAP groups of 64 children: which lanes hold a ring slot */
+    float4 *ring;         /* PT_RCAP child slots: parked ray, then the child's term      */
     unsigned char *fastq; /* PT_SCAP slots waiting for the fast pass (position mod 256) */
     unsigned char *slowq; /* PT_SCAP slots waiting for the full merge                   */
 };
@@ -1112,8 +1111,7 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #define PT_KATT 2 /* rejection attempts per lane per generation round */
 #endif
 #define PT_QCAP 256 /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
-#define PT_RCAP 256 /* kept-child slots per wave awaiting their group sum          */
-#define PT_GCAP 32  /* groups per wave awaiting their sum                           */
+#define PT_RCAP 256 /* child slots per wave awaiting their group sum               */
 #define PT_SCAP 256 /* parked children per queue (byte offsets): a drain can add 2 x 64 to < 64 */
 static_assert(64 + 64 * PT_KATT <= PT_QCAP, "queue too small for PT_KATT");
 #define PT_JUMP_ENTRIES 193 /* host table: m = 0..192 attempts (PT_KATT <= 3) */
@@ -1252,20 +1250,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const u64 A64 = jump[128], g64inc = jump[129] * rng.inc;   /* 64 attempts = 192 draws  */
     const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * rng.inc; /* a full round */
     int qhead = 0, qn = 0, fails = 0, reason = -1;
-    /* children are numbered in stage-A order (npos); stage A's batches of 64 are
-     * the summation groups.  A DARK child (no emissive primitive reachable, and a
-     * positive weight) has the burst-uniform term Z = rc * 0 and takes no ring
-     * slot; every other child is KEPT in the slot ring (numbered nkeep), and each
-     * group records which of its lanes were kept (gmask). */
-    int npos = 0, f_head = 0, f_n = 0, s_head = 0, s_n = 0;
-    int nkeep = 0, keep_sum = 0, ngrp = 0, gsum = 0;
-    /* register copies of LDS queue heads: ring number of the first entry of
-     * fastq / slowq (valid while non-empty) and the oldest unsummed group's mask */
-    int f_first = 0, s_first = 0;
-    u64 head_gm = 0ull;
-    u64 *const gmask = L.gmask;
-    /* ((aN * factor) * rc) * (+0) == rc * (+0) bitwise for any finite aN * factor > 0 */
-    const V3 Z = rc * mk(0.0f, 0.0f, 0.0f);
+    int npos = 0, sum_ptr = 0, f_head = 0, f_n = 0, s_head = 0, s_n = 0; /* slot ring / queue positions */
     int fast_on = 1;
     u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
     PT_CNT(cnt, 0, 1);
@@ -1346,8 +1331,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
              * queue for the fast pass. */
             const int cntb = qn < 64 ? qn : 64;
             PT_CNT(cnt, 2, 1);
-            int lit = 0, keep = 0;
-            float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            int lit = 0;
             if (lane < cntb) {
                 float4 en = q[(qhead + lane) & (PT_QCAP - 1)];
                 V3 dir = mk(en.x, en.y, en.z);
@@ -1355,13 +1339,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     dir = cnormalize(dir);
                     en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
                 }
+                float4 out;
 #if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
                 /* experiment: generation cost only */
                 {
                     const V3 col = dir.z < 0.0f ? S::emis(0, hit + dir, e) : mk(0, 0, 0);
                     const V3 term = ((aN * en.w) * rc) * col;
                     out = make_float4(term.x, term.y, term.z, 0.0f);
-                    keep = 1;
                 }
 #else
                 {
@@ -1376,29 +1360,16 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 }
                 if (lit) {
                     out = make_float4(dir.x, dir.y, dir.z, en.w);
-                    keep = 1;
-                } else if (!(en.w > 0.0f)) {
-                    /* not provably Z: keep the exact term */
+                } else {
                     const V3 term = ((aN * en.w) * rc) * mk(0.0f, 0.0f, 0.0f);
                     out = make_float4(term.x, term.y, term.z, 0.0f);
-                    keep = 1;
                 }
 #endif
+                ring[(npos + lane) & (PT_RCAP - 1)] = out;
             }
-            const u64 KM = __ballot(keep), LM = __ballot(lit);
-            const int kidx = nkeep + __popcll(KM & below);
-            if (keep)
-                ring[kidx & (PT_RCAP - 1)] = out;
+            const u64 LM = __ballot(lit);
             if (lit)
-                fastq[(f_head + f_n + __popcll(LM & below)) & (PT_SCAP - 1)] = (unsigned char)kidx;
-            if (lane == 0)
-                gmask[ngrp & (PT_GCAP - 1)] = KM;
-            if (gsum == ngrp)
-                head_gm = KM;
-            if (f_n == 0 && LM)
-                f_first = nkeep + __popcll(KM & ((1ull << __builtin_ctzll(LM)) - 1ull));
-            ngrp++;
-            nkeep += __popcll(KM);
+                fastq[(f_head + f_n + __popcll(LM & below)) & (PT_SCAP - 1)] = (unsigned char)(npos + lane);
             f_n += __popcll(LM);
             n_dark += (u32)(cntb - __popcll(LM));
             npos += cntb;
@@ -1409,11 +1380,10 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             PT_ACC(cnt, 1, ta);
         }
         const bool final = reason >= 0 && qn == 0;
-        /* queued slots hold ring numbers mod 256; every pending one lies in
-         * [keep_sum, keep_sum + PT_RCAP), which restores it */
-        auto slot_pos = [&](unsigned char v) { return keep_sum + ((int)(v - keep_sum) & (PT_RCAP - 1)); };
-        /* drain everything when the next stage-A batch might not fit */
-        const bool pressure = nkeep - keep_sum > PT_RCAP - 64 || ngrp - gsum > PT_GCAP - 2;
+        /* queued slots hold positions mod 256; every pending position lies in
+         * [sum_ptr, sum_ptr + PT_RCAP), which restores it */
+        auto slot_pos = [&](unsigned char v) { return sum_ptr + ((int)(v - sum_ptr) & (PT_RCAP - 1)); };
+        const bool pressure = npos - sum_ptr > PT_RCAP - 64;
         PT_T0(tb);
         /* ---- stage B: fast pass over 64 parked children.  Lanes whose spans
          * pass the fast check finish; the others stay parked for the full merge */
@@ -1454,8 +1424,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             const u64 SM = __ballot(slow);
             if (slow)
                 slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = (unsigned char)pos;
-            if (s_n == 0 && SM)
-                s_first = __builtin_amdgcn_readlane(pos, __builtin_ctzll(SM));
             s_n += __popcll(SM);
             n_slow += (u32)__popcll(SM);
             /* overlap-heavy scenes (e.g. a box of sky half-spaces) stop trying */
@@ -1463,8 +1431,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 fast_on = 0;
             f_head += cf;
             f_n -= cf;
-            if (f_n)
-                f_first = slot_pos(uni(fastq[f_head & (PT_SCAP - 1)]));
         }
         PT_ACC(cnt, 2, tb);
         PT_T0(tc);
@@ -1491,35 +1457,23 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             }
             s_head += cs;
             s_n -= cs;
-            if (s_n)
-                s_first = slot_pos(uni(slowq[s_head & (PT_SCAP - 1)]));
         }
         PT_ACC(cnt, 3, tc);
         PT_T0(ts);
         /* ---- sum finished groups in order: 64 children per group (the last
-         * group of a burst may be shorter), group-64 tree or sequential; a
-         * group is finished when every kept child in it has its term */
+         * group of a burst may be shorter), group-64 tree or sequential */
         {
-            int resolved = nkeep;
+            int resolved = npos;
             if (s_n)
-                resolved = s_first;
+                resolved = slot_pos(uni(slowq[s_head & (PT_SCAP - 1)]));
             if (f_n)
-                resolved = min(resolved, f_first);
-            while (gsum < ngrp) {
-                const u64 gm = head_gm;
-                const int gk = __popcll(gm);
-                if (keep_sum + gk > resolved)
-                    break;
-                u64 nx = 0ull;
-                if (gsum + 1 < ngrp)
-                    nx = gmask[(gsum + 1) & (PT_GCAP - 1)];
-                const int cg = min(64, npos - 64 * gsum);
+                resolved = min(resolved, slot_pos(uni(fastq[f_head & (PT_SCAP - 1)])));
+            while (sum_ptr < resolved && (resolved - sum_ptr >= 64 || (final && s_n == 0 && f_n == 0))) {
+                const int cg = (npos - sum_ptr) < 64 ? (npos - sum_ptr) : 64;
                 PT_CNT(cnt, 5, 1);
                 V3 term = mk(-0.0f, -0.0f, -0.0f);
-                if (lane < cg)
-                    term = Z;
-                if ((gm >> lane) & 1ull) {
-                    const float4 tv = ring[(keep_sum + __popcll(gm & below)) & (PT_RCAP - 1)];
+                if (lane < cg) {
+                    const float4 tv = ring[(sum_ptr + lane) & (PT_RCAP - 1)];
                     term = mk(tv.x, tv.y, tv.z);
                 }
                 if (STRICT) {
@@ -1529,9 +1483,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     retval = retval + mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
                     retval = univ(retval);
                 }
-                keep_sum += gk;
-                gsum++;
-                head_gm = ((u64)(u32)uni((int)(nx >> 32)) << 32) | (u64)(u32)uni((int)nx);
+                sum_ptr += cg;
             }
         }
         PT_ACC(cnt, 4, ts);
@@ -1744,7 +1696,6 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     __shared__ Frame stk[PT_WPW][MAXD + 1];
     __shared__ float4 qbuf[PT_WPW][PT_QCAP];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
-    __shared__ u64 gbuf[PT_WPW][PT_GCAP];
     __shared__ unsigned char fbuf[PT_WPW][PT_SCAP];
     __shared__ unsigned char sbuf[PT_WPW][PT_SCAP];
     __shared__ Counters cbuf[PT_WPW];
@@ -1759,7 +1710,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
 #endif
-    const WaveLds L = {qbuf[wave], rbuf[wave], gbuf[wave], fbuf[wave], sbuf[wave]};
+    const WaveLds L = {qbuf[wave], rbuf[wave], fbuf[wave], sbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
@@ -1915,4 +1866,3 @@ extern "C" __global__ void pt_selftest_math(u64 n, u64 seed, unsigned long long 
         atomicAdd(&bad[2], bn);
 }
 #endif
-)PTDEV"
