@@ -1579,21 +1579,36 @@ enum { RS_REFRACT, RS_SCATTER };
 
 /* One sample = one traceRay tree (path-trace.h:58-165) + the jittered camera
  * ray of tracePixel (path-trace.h:190-198).  F = this wave's frame stack. */
+/* The camera query of a sample, found ahead of time by one lane of the wave
+ * (render_chunk traces a chunk's camera rays one per lane). */
+struct CamHit
+{
+    int hit;
+    float t;
+    u32 ref;
+    int ex;
+};
+
+/* tracePixel's jittered camera ray (path-trace.h:190-198): two draws */
+__device__ __forceinline__ V3 camera_dir(const PtLaunch &lp, int pix, Rng &rng)
+{
+    const int px = pix % lp.gw, py = pix / lp.gw;
+    float x = 2.0f * ((float)px + u01(rng_next(rng))) / (float)lp.W - 1.0f;
+    float y = 1.0f - 2.0f * ((float)py + u01(rng_next(rng))) / (float)lp.H;
+    return mk(x * lp.sw, y * lp.sh, -lp.dist);
+}
+
 template <class S, int MAXD, bool STRICT>
 __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, const WaveLds &L,
-                                           const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt)
+                                           const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt,
+                                           const CamHit &cam)
 {
     Rng rng;
     rng_seed(rng, lp.seed, (u64)pix, (u64)s);
-    const int px = pix % lp.gw, py = pix / lp.gw;
-    {
-        float x = 2.0f * ((float)px + u01(rng_next(rng))) / (float)lp.W - 1.0f;
-        float y = 1.0f - 2.0f * ((float)py + u01(rng_next(rng))) / (float)lp.H;
-        F[0].o = mk(0, 0, 0);
-        F[0].d = mk(x * lp.sw, y * lp.sh, -lp.dist);
-        F[0].strength = 1.0f;
-        F[0].depth = lp.depth;
-    }
+    F[0].o = mk(0, 0, 0);
+    F[0].d = camera_dir(lp, pix, rng);
+    F[0].strength = 1.0f;
+    F[0].depth = lp.depth;
     int sp = 0;
     int phase = PH_ENTER;
     V3 result = mk(0, 0, 0);
@@ -1602,12 +1617,18 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
         if (phase == PH_ENTER) {
             cnt.queries++;
             const V3 o = univ(f.o), d = univ(f.d);
-            typename S::Root::Ctx ctx;
-            S::Root::prep(ctx, o, e);
             float t = 0.0f;
             u32 ref = 0;
             bool ex = false;
-            if (!first_hit<typename S::Root>(ctx, d, e, t, ref, ex)) {
+            bool found;
+            if (sp == 0) {
+                found = cam.hit != 0, t = cam.t, ref = cam.ref, ex = cam.ex != 0;
+            } else {
+                typename S::Root::Ctx ctx;
+                S::Root::prep(ctx, o, e);
+                found = first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+            }
+            if (!found) {
                 result = mk(0, 0, 0);
                 phase = PH_RETURN;
                 continue;
@@ -1771,6 +1792,22 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         if (chunk >= n_chunks)
             break;
         const long long item0 = chunk * CH;
+        /* the chunk's camera queries, one per lane */
+        CamHit ch = {0, 0.0f, 0u, 0};
+        if (lane < CH && item0 + lane < lp.n_items) {
+            const long long item = item0 + lane;
+            const long long slot = item / lp.nsamp;
+            const int s = lp.s0 + (int)(item - slot * lp.nsamp);
+            const int pix = pixels ? pixels[slot] : (int)slot;
+            Rng r;
+            rng_seed(r, lp.seed, (u64)pix, (u64)s);
+            const V3 d = camera_dir(lp, pix, r);
+            typename S::Root::Ctx ctx;
+            S::Root::prep(ctx, mk(0, 0, 0), e);
+            bool ex = false;
+            ch.hit = first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
+            ch.ex = ex ? 1 : 0;
+        }
         V3 mine = mk(0, 0, 0);
         for (int j = 0; j < CH; j++) {
             const long long item = item0 + j;
@@ -1780,8 +1817,10 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             const int s = lp.s0 + (int)(item - slot * lp.nsamp);
             const int pix = pixels ? pixels[slot] : (int)slot;
             PT_T0(tt);
+            const CamHit cam = {__builtin_amdgcn_readlane(ch.hit, j), rdlane(ch.t, j),
+                                (u32)__builtin_amdgcn_readlane((int)ch.ref, j), __builtin_amdgcn_readlane(ch.ex, j)};
             V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], L, jump, A3l, G3l,
-                                                 cnt);
+                                                 cnt, cam);
             PT_ACC(cnt, 6, tt);
             if (lane == j)
                 mine = c;
@@ -1814,7 +1853,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
 } // namespace ptd
 
 #ifndef PT_MIN_WAVES
-#define PT_MIN_WAVES 1
+#define PT_MIN_WAVES 4 /* 4 workgroups of 4 waves per CU: caps VGPRs at 128 (4 waves/SIMD) */
 #endif
 
 #define PT_RENDER_ARGS                                                                                     \
