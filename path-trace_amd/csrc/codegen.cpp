@@ -12,6 +12,7 @@
 #include <map>
 #include <fstream>
 #include <sstream>
+#include <vector>
 
 #include "internal.h"
 
@@ -241,6 +242,7 @@ Generated generate(const SceneImpl &s, int depth)
     /* dark(m): material m's emission is the constant (+0, +0, +0), so a leaf
      * child whose first hit is m (or a miss) contributes weight * +0 */
     src << "  __device__ static constexpr bool dark(int m) { return ";
+    std::vector<int> lit_mats;
     for (size_t k = 0; k < g.mats.size(); k++) {
         const TexRec &e = s.textures.at(s.materials.at(g.mats[k]).emissive);
         bool z = e.kind == TexKind::Color;
@@ -249,10 +251,22 @@ Generated generate(const SceneImpl &s, int depth)
             memcpy(&bits, &e.f[c], 4);
             z = bits == 0u;
         }
+        if (!z)
+            lit_mats.push_back((int)k);
         src << "m == " << k << " ? " << (z ? "true" : "false") << " : ";
     }
     src << "false; }\n";
-    if (all_emis_const) {
+    if (all_emis_const && lit_mats.size() <= 4) {
+        /* few constant emitters: a select chain on scalar-loaded constants
+         * (dark materials keep the exact (+0, +0, +0)) instead of a per-lane
+         * table load */
+        src << "  __device__ static __forceinline__ V3 emis(int m, V3, const Env &e) {\n"
+            << "    V3 r = mk(0.0f, 0.0f, 0.0f);\n";
+        for (int k : lit_mats)
+            src << "    r = m == " << k << " ? mk(e.P[" << emis_tab + 3 * k << "], e.P[" << emis_tab + 3 * k + 1
+                << "], e.P[" << emis_tab + 3 * k + 2 << "]) : r;\n";
+        src << "    return r;\n  }\n";
+    } else if (all_emis_const) {
         src << "  __device__ static __forceinline__ V3 emis(int m, V3, const Env &e) {\n"
             << "    const float *t = e.P + " << emis_tab << " + 3 * m;\n    return mk(t[0], t[1], t[2]);\n  }\n";
     } else {
