@@ -29,6 +29,7 @@
 #ifndef PT_PATHTRACE_HPP
 #define PT_PATHTRACE_HPP
 
+#include <cctype>
 #include <cmath>
 #include <map>
 #include <memory>
@@ -183,14 +184,29 @@ class Image
 {
 public:
     Image() {}
+    /* src/image.cpp:49-83: format from the extension unless given; "png" or
+     * "hdr"/"pic" */
     explicit Image(std::string fileName, std::string format = "")
     {
-        (void)format; /* only Radiance HDR is decoded (PNG needs libpng) */
+        if (format.empty()) {
+            size_t dot = fileName.find_last_of('.');
+            if (dot == std::string::npos)
+                throw ImageLoadError("can't determine format");
+            format = fileName.substr(dot + 1);
+        }
+        for (auto &c : format) c = (char)tolower((unsigned char)c);
+        int (*rd)(const char *, float *, int *, int *);
+        if (format == "png")
+            rd = pt_png_read;
+        else if (format == "hdr" || format == "pic")
+            rd = pt_hdr_read;
+        else
+            throw ImageLoadError("invalid format"); /* src/image.cpp:327 */
         int w = 0, h = 0;
-        if (pt_hdr_read(fileName.c_str(), nullptr, &w, &h) != PT_OK)
+        if (rd(fileName.c_str(), nullptr, &w, &h) != PT_OK)
             throw ImageLoadError(pt_last_error());
         std::shared_ptr<std::vector<float>> px(new std::vector<float>((size_t)w * h * 4));
-        if (pt_hdr_read(fileName.c_str(), px->data(), &w, &h) != PT_OK)
+        if (rd(fileName.c_str(), px->data(), &w, &h) != PT_OK)
             throw ImageLoadError(pt_last_error());
         data_ = px, w_ = (unsigned)w, h_ = (unsigned)h;
     }

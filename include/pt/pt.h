@@ -47,12 +47,22 @@ const char *pt_version(void);
 /* ------------------------------------------------------------- images --- */
 /* Image(string fileName) for ".hdr"/".pic" (reference src/image.cpp:83-324). */
 pt_id pt_image_load_hdr(pt_scene *s, const char *path);
+/* Image(string fileName) for ".png": PngDecoder (reference src/png_decoder.cpp:
+ * 40-128) + byte / 255.0f (src/image.cpp:60-79); RGB gets alpha 0 (the
+ * png_set_filler(0) of :94-97), palette tRNS becomes alpha.  Grayscale PNGs
+ * are PT_ERR_IO (the reference's decoder leaves their rows half written). */
+pt_id pt_image_load_png(pt_scene *s, const char *path);
+/* Image(string fileName) with the format taken from the extension
+ * (src/image.cpp:49-59): "png", "hdr", "pic" (case-insensitive). */
+pt_id pt_image_load(pt_scene *s, const char *path);
 /* MutableImage -> Image (include/image.h:110-211): rgba is h rows of w RGBA
  * floats, row 0 = top; copied. */
 pt_id pt_image_from_rgba32f(pt_scene *s, const float *rgba, int w, int h);
 /* Decode a Radiance HDR file into caller memory (w*h*4 floats); pass
  * rgba=NULL to query the size. */
 int pt_hdr_read(const char *path, float *rgba, int *w, int *h);
+/* The same for a PNG file (pt_image_load_png's decoding). */
+int pt_png_read(const char *path, float *rgba, int *w, int *h);
 
 /* ----------------------------------------------------------- textures --- */
 pt_id pt_tex_color(pt_scene *s, float r, float g, float b);              /* ColorTexture       texture.h:29-58  */

@@ -49,7 +49,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     cmd = ["hipcc", "--offload-arch=gfx950", "-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
            "-Wall", "-Wno-unused-result", "-o", LIB + ".tmp"]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
-    cmd += ["-ldl"]  # hiprtc is dlopen'ed by path (csrc/jit.cpp)
+    cmd += ["-ldl", "-lz"]  # hiprtc is dlopen'ed by path (csrc/jit.cpp); zlib for PNG
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -2,15 +2,24 @@
  * imageio.cpp -- the output and environment-map formats of the reference:
  *   read_hdr  : Radiance RGBE reader (reference src/image.cpp:83-324),
  *               new-style RLE scanlines, 179 * 2^(e-136) scaling, alpha 1;
+ *   read_png  : PngDecoder (src/png_decoder.cpp:40-128, libpng) restated on
+ *               zlib: 8/16-bit RGB(A) and 1-8-bit palette images, Adam7,
+ *               then Image::Image's byte / 255.0f (src/image.cpp:60-79);
+ *   read_image: Image(string fileName) format dispatch by extension;
  *   write_hdr : MutableImage::writeHDR (src/image.cpp:398-481), byte-for-byte
  *               the same greedy run/literal encoder;
  *   write_bmp : the 24-bpp BI_RGB bottom-up BMP that SDL_SaveBMP wrote for the
  *               demo (src/test.cpp:1037-1059), bytes clamp(floor(256*c/count)).
  */
+#include <zlib.h>
+
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 
 #include "internal.h"
 
@@ -170,6 +179,221 @@ ImageRec read_hdr(const std::string &path)
         img.rgba[i + 3] = 1;
     }
     return img;
+}
+
+/* ------------------------------------------------------------------ PNG --
+ * PngDecoder (reference src/png_decoder.cpp:40-128) + the /255 conversion of
+ * Image::Image (src/image.cpp:60-79).  The reference drives libpng with
+ * png_set_strip_16 (keep the high byte), png_set_packing, for palette images
+ * png_set_palette_to_rgb (expands the palette and, libpng >= 1.2.9, tRNS to
+ * alpha), and png_set_filler(0, AFTER) when the colour type has no alpha;
+ * png_read_image deinterlaces Adam7.  Rows land in a w*4-byte-per-row RGBA
+ * buffer.  Grayscale colour types come out as 1-2 bytes per pixel in that
+ * 4-byte-per-pixel buffer (rows half written, the rest uninitialised), which
+ * no decoder can reproduce, so they are rejected here. */
+namespace
+{
+
+uint32_t be32(const uint8_t *p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+int paeth(int a, int b, int c)
+{
+    int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+    if (pa <= pb && pa <= pc)
+        return a;
+    return pb <= pc ? b : c;
+}
+
+/* Reverses the scanline filters of one (sub)image in place: rows of 1 + rb bytes. */
+void unfilter(uint8_t *data, size_t rows, size_t rb, int bpp)
+{
+    std::vector<uint8_t> zero(rb, 0);
+    const uint8_t *prev = zero.data();
+    for (size_t y = 0; y < rows; y++) {
+        uint8_t *row = data + y * (rb + 1);
+        const int f = row[0];
+        uint8_t *x = row + 1;
+        switch (f) {
+        case 0:
+            break;
+        case 1:
+            for (size_t i = bpp; i < rb; i++) x[i] = (uint8_t)(x[i] + x[i - bpp]);
+            break;
+        case 2:
+            for (size_t i = 0; i < rb; i++) x[i] = (uint8_t)(x[i] + prev[i]);
+            break;
+        case 3:
+            for (size_t i = 0; i < rb; i++) x[i] = (uint8_t)(x[i] + ((i >= (size_t)bpp ? x[i - bpp] : 0) + prev[i]) / 2);
+            break;
+        case 4:
+            for (size_t i = 0; i < rb; i++)
+                x[i] = (uint8_t)(x[i] + paeth(i >= (size_t)bpp ? x[i - bpp] : 0, prev[i], i >= (size_t)bpp ? prev[i - bpp] : 0));
+            break;
+        default:
+            throw Error(PT_ERR_IO, "bad adaptive filter value");
+        }
+        prev = x;
+    }
+}
+
+} // namespace
+
+ImageRec read_png(const std::string &path)
+{
+    std::ifstream is(path, std::ios::binary);
+    if (!is)
+        throw Error(PT_ERR_IO, "can't open file : \"" + path + "\"");
+    std::vector<uint8_t> file((std::istreambuf_iterator<char>(is)), std::istreambuf_iterator<char>());
+    static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    if (file.size() < 8 || memcmp(file.data(), sig, 8) != 0)
+        throw Error(PT_ERR_IO, "Not a PNG file");
+    uint32_t w = 0, h = 0;
+    int depth = 0, ctype = -1, interlace = 0;
+    std::vector<uint8_t> plte, trns, idat;
+    bool end = false;
+    for (size_t p = 8; !end;) {
+        if (p + 12 > file.size())
+            throw Error(PT_ERR_IO, "Read Error");
+        const uint32_t len = be32(&file[p]);
+        if (len > 0x7fffffffu || p + 12 + (size_t)len > file.size())
+            throw Error(PT_ERR_IO, "Read Error");
+        const uint8_t *type = &file[p + 4], *d = &file[p + 8];
+        const bool critical = !(type[0] & 0x20);
+        const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), type, 4 + len);
+        if (crc != be32(d + len)) {
+            if (critical)
+                throw Error(PT_ERR_IO, std::string((const char *)type, 4) + ": CRC error");
+            p += 12 + (size_t)len; /* ancillary: libpng warns and discards */
+            continue;
+        }
+        const std::string t((const char *)type, 4);
+        if (t == "IHDR") {
+            if (len != 13)
+                throw Error(PT_ERR_IO, "Invalid IHDR chunk");
+            w = be32(d), h = be32(d + 4), depth = d[8], ctype = d[9], interlace = d[12];
+            if (w == 0 || h == 0 || w > 0x7fffffffu / 4 || h > 0x7fffffffu / 4 || d[10] != 0 || d[11] != 0 || interlace > 1)
+                throw Error(PT_ERR_IO, "Invalid IHDR data");
+        } else if (t == "PLTE") {
+            plte.assign(d, d + len);
+        } else if (t == "tRNS") {
+            trns.assign(d, d + len);
+        } else if (t == "IDAT") {
+            idat.insert(idat.end(), d, d + len);
+        } else if (t == "IEND") {
+            end = true;
+        }
+        p += 12 + (size_t)len;
+    }
+    if (ctype < 0)
+        throw Error(PT_ERR_IO, "Missing IHDR before IDAT");
+    int channels;
+    switch (ctype) {
+    case 2: channels = 3; break;
+    case 3: channels = 1; break;
+    case 6: channels = 4; break;
+    case 0:
+    case 4: throw Error(PT_ERR_IO, "grayscale PNG: the reference decoder leaves rows partly unwritten");
+    default: throw Error(PT_ERR_IO, "Invalid color type in IHDR");
+    }
+    const bool ok_depth = ctype == 3 ? (depth == 1 || depth == 2 || depth == 4 || depth == 8) : (depth == 8 || depth == 16);
+    if (!ok_depth)
+        throw Error(PT_ERR_IO, "Invalid bit depth in IHDR");
+    if (ctype == 3 && (plte.empty() || plte.size() % 3 != 0))
+        throw Error(PT_ERR_IO, "Missing PLTE before IDAT");
+    const int bits = channels * depth, bpp = std::max(1, bits / 8);
+
+    /* Adam7 passes (or the whole image) */
+    struct Pass
+    {
+        int x0, y0, dx, dy;
+    };
+    static const Pass adam7[7] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4},
+                                  {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
+    const Pass whole = {0, 0, 1, 1};
+    const int npass = interlace ? 7 : 1;
+    size_t raw_size = 0;
+    for (int k = 0; k < npass; k++) {
+        const Pass &ps = interlace ? adam7[k] : whole;
+        const size_t pw = (w + ps.dx - 1 - ps.x0) / ps.dx, ph = (h + ps.dy - 1 - ps.y0) / ps.dy;
+        if (w <= (uint32_t)ps.x0 || h <= (uint32_t)ps.y0 || pw == 0 || ph == 0)
+            continue;
+        raw_size += ph * (1 + (pw * bits + 7) / 8);
+    }
+    std::vector<uint8_t> raw(raw_size);
+    {
+        z_stream zs;
+        memset(&zs, 0, sizeof zs);
+        if (inflateInit(&zs) != Z_OK)
+            throw Error(PT_ERR_IO, "zlib init failed");
+        zs.next_in = idat.data();
+        zs.avail_in = (uInt)idat.size();
+        zs.next_out = raw.data();
+        zs.avail_out = (uInt)raw.size();
+        const int rc = inflate(&zs, Z_FINISH);
+        const size_t got = raw.size() - zs.avail_out;
+        inflateEnd(&zs);
+        if ((rc != Z_STREAM_END && !(rc == Z_BUF_ERROR && zs.avail_out == 0)) || got != raw.size())
+            throw Error(PT_ERR_IO, rc == Z_DATA_ERROR ? "Decompression error" : "Not enough image data");
+    }
+    ImageRec img;
+    img.w = (int)w, img.h = (int)h;
+    img.rgba.assign((size_t)4 * w * h, 0.0f);
+    auto sample = [&](const uint8_t *row, size_t x, int c) -> int { /* 8-bit value after strip_16 / packing */
+        if (depth == 16)
+            return row[(x * channels + c) * 2];
+        if (depth == 8)
+            return row[x * channels + c];
+        const size_t bit = x * depth;
+        return (row[bit / 8] >> (8 - depth - (int)(bit % 8))) & ((1 << depth) - 1);
+    };
+    size_t off = 0;
+    for (int k = 0; k < npass; k++) {
+        const Pass &ps = interlace ? adam7[k] : whole;
+        if (w <= (uint32_t)ps.x0 || h <= (uint32_t)ps.y0)
+            continue;
+        const size_t pw = (w + ps.dx - 1 - ps.x0) / ps.dx, ph = (h + ps.dy - 1 - ps.y0) / ps.dy;
+        const size_t rb = (pw * bits + 7) / 8;
+        unfilter(&raw[off], ph, rb, bpp);
+        for (size_t py = 0; py < ph; py++) {
+            const uint8_t *row = &raw[off + py * (rb + 1) + 1];
+            const size_t y = ps.y0 + py * ps.dy;
+            for (size_t px = 0; px < pw; px++) {
+                const size_t x = ps.x0 + px * ps.dx;
+                uint8_t out[4];
+                if (ctype == 3) {
+                    const int i = sample(row, px, 0);
+                    if ((size_t)(3 * i + 2) < plte.size()) {
+                        out[0] = plte[3 * i], out[1] = plte[3 * i + 1], out[2] = plte[3 * i + 2];
+                    } else {
+                        out[0] = out[1] = out[2] = 0; /* index past the palette: libpng zero-fills */
+                    }
+                    out[3] = trns.empty() ? 0 : ((size_t)i < trns.size() ? trns[i] : 255);
+                } else {
+                    for (int c = 0; c < channels; c++) out[c] = (uint8_t)sample(row, px, c);
+                    if (channels == 3)
+                        out[3] = 0; /* png_set_filler(0, PNG_FILLER_AFTER) */
+                }
+                float *o = &img.rgba[4 * (y * w + x)];
+                for (int c = 0; c < 4; c++) o[c] = (int)out[c] / 255.0f;
+            }
+        }
+        off += ph * (rb + 1);
+    }
+    return img;
+}
+
+ImageRec read_image(const std::string &path)
+{
+    const size_t dot = path.find_last_of('.');
+    if (dot == std::string::npos)
+        throw Error(PT_ERR_IO, "can't determine format");
+    std::string fmt = path.substr(dot + 1);
+    for (auto &c : fmt) c = (char)tolower((unsigned char)c);
+    if (fmt == "png")
+        return read_png(path);
+    if (fmt == "hdr" || fmt == "pic")
+        return read_hdr(path);
+    throw Error(PT_ERR_IO, "invalid format"); /* src/image.cpp:327 */
 }
 
 void write_hdr(const std::string &path, const float *rgb, int w, int h)

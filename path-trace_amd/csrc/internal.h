@@ -99,6 +99,8 @@ void mat_rotate(const float *axis, double angle, float *out);
 
 /* Image I/O (reference src/image.cpp). */
 ImageRec read_hdr(const std::string &path);
+ImageRec read_png(const std::string &path);
+ImageRec read_image(const std::string &path);
 void write_hdr(const std::string &path, const float *rgb, int w, int h);
 void write_bmp(const std::string &path, const float *rgb, int w, int h, int count);
 

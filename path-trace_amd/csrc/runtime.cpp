@@ -311,6 +311,9 @@ void load_text(SceneImpl &s, const std::string &text)
             if (ty == "hdr") {
                 need(t, 4);
                 s.images.push_back(read_hdr(t[3]));
+            } else if (ty == "png") {
+                need(t, 4);
+                s.images.push_back(read_png(t[3]));
             } else if (ty == "raw") {
                 need(t, 6);
                 ImageRec r;
@@ -681,6 +684,24 @@ pt_id pt_image_load_hdr(pt_scene *s, const char *path)
     });
 }
 
+pt_id pt_image_load_png(pt_scene *s, const char *path)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        sc.images.push_back(read_png(path ? path : ""));
+        return (int)sc.images.size() - 1;
+    });
+}
+
+pt_id pt_image_load(pt_scene *s, const char *path)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        sc.images.push_back(read_image(path ? path : ""));
+        return (int)sc.images.size() - 1;
+    });
+}
+
 pt_id pt_image_from_rgba32f(pt_scene *s, const float *rgba, int w, int h)
 {
     return guard([&] {
@@ -692,6 +713,20 @@ pt_id pt_image_from_rgba32f(pt_scene *s, const float *rgba, int w, int h)
         r.rgba.assign(rgba, rgba + (size_t)4 * w * h);
         sc.images.push_back(std::move(r));
         return (int)sc.images.size() - 1;
+    });
+}
+
+int pt_png_read(const char *path, float *rgba, int *w, int *h)
+{
+    return guard([&] {
+        ImageRec r = read_png(path ? path : "");
+        if (w)
+            *w = r.w;
+        if (h)
+            *h = r.h;
+        if (rgba)
+            memcpy(rgba, r.rgba.data(), r.rgba.size() * 4);
+        return PT_OK;
     });
 }
 

@@ -18,7 +18,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import PT_ORDER_GROUP64, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, load_hdr, \
+from ._lib import PT_ORDER_GROUP64, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, load_hdr, load_png, \
     write_bmp, write_hdr
 from .scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTexture, ImageSkyboxAlphaTexture,
                     ImageSkyboxTexture, ImageTexture, Intersection, LogTexture, Material, Matrix,

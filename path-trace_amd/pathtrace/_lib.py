@@ -56,8 +56,11 @@ SIGNATURES = {
     "pt_last_error": (ctypes.c_char_p, []),
     "pt_version": (ctypes.c_char_p, []),
     "pt_image_load_hdr": (_I, [_P, ctypes.c_char_p]),
+    "pt_image_load_png": (_I, [_P, ctypes.c_char_p]),
+    "pt_image_load": (_I, [_P, ctypes.c_char_p]),
     "pt_image_from_rgba32f": (_I, [_P, _P, _I, _I]),
     "pt_hdr_read": (_I, [ctypes.c_char_p, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "pt_png_read": (_I, [ctypes.c_char_p, _P, ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "pt_tex_color": (_I, [_P, _F, _F, _F]),
     "pt_tex_image": (_I, [_P, _I]),
     "pt_tex_image_alpha": (_I, [_P, _I]),
@@ -151,13 +154,23 @@ def selftest_math(n: int = 1 << 26, seed: int = 1, device: int = 0):
     return dict(zip(["sqrt", "div", "normalize"], [int(v) for v in out]))
 
 
-def load_hdr(path: str) -> np.ndarray:
+def _read(fn, path: str) -> np.ndarray:
     w = ctypes.c_int(0)
     h = ctypes.c_int(0)
-    check(lib().pt_hdr_read(path.encode(), None, ctypes.byref(w), ctypes.byref(h)))
+    check(fn(path.encode(), None, ctypes.byref(w), ctypes.byref(h)))
     out = np.zeros((h.value, w.value, 4), dtype=np.float32)
-    check(lib().pt_hdr_read(path.encode(), out.ctypes.data, ctypes.byref(w), ctypes.byref(h)))
+    check(fn(path.encode(), out.ctypes.data, ctypes.byref(w), ctypes.byref(h)))
     return out
+
+
+def load_hdr(path: str) -> np.ndarray:
+    """Radiance HDR decode (reference src/image.cpp:83-324): h x w x RGBA float32."""
+    return _read(lib().pt_hdr_read, path)
+
+
+def load_png(path: str) -> np.ndarray:
+    """PNG decode as the reference's Image(fileName) (src/image.cpp:60-79): h x w x RGBA float32."""
+    return _read(lib().pt_png_read, path)
 
 
 def write_hdr(path: str, rgb: np.ndarray) -> None:

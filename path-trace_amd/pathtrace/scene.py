@@ -131,8 +131,15 @@ class Image:
 
     def __init__(self, data=None, path: Optional[str] = None):
         if path is not None:
+            # Image(string fileName): format from the extension (src/image.cpp:49-83)
             from . import _lib
-            data = _lib.load_hdr(path)
+            ext = path.rsplit(".", 1)[-1].lower() if "." in path else ""
+            if ext == "png":
+                data = _lib.load_png(path)
+            elif ext in ("hdr", "pic"):
+                data = _lib.load_hdr(path)
+            else:
+                raise _lib.PtError("can't determine format" if not ext else "invalid format")
         if data is None:
             raise ValueError("Image needs data or a path")
         data = np.ascontiguousarray(data, dtype=np.float32)
