@@ -6,26 +6,25 @@
  * and only requires `unsigned operator()()`, `static min()`, `static max()`
  * (consumed by uniform_real_distribution, include/vector3d.h:14-34).  Its own
  * DefaultRandomEngine (include/path-trace.h:21-54) is one global, racy LCG
- * whose streams for adjacent seeds are nearly identical, so it cannot give
- * per-sample reproducibility.  This header defines the engine that the GPU
- * megakernel, the CPU oracle and the golden generator all plug into `T`:
+ * whose 32-bit seed() gives adjacent seeds nearly identical streams, so it
+ * cannot give per-sample reproducibility.  This header keeps the reference
+ * engine's RECURRENCE and output exactly and only replaces its seeding:
  *
- *   PCG32 (XSH-RR 64/32).  state' = state * PT_PCG_MULT + inc (mod 2^64);
- *   output = rotr32(((old ^ (old >> 18)) >> 27), old >> 59).
+ *   v' = 214013 * v + 2531011  (mod 2^64),  output = (unsigned)(v' >> 32)
+ *     (DefaultRandomEngine::operator(), include/path-trace.h:45-49)
  *
- * Each (pixel, sample) owns a private stream:
- *   key   = splitmix64(run_seed) ^ (pixel_index << 20) ^ sample_index
- *   state = splitmix64(key)
- *   inc   = (splitmix64(key ^ PT_STREAM_SALT) << 1) | 1
+ * with a private starting state per (pixel, sample):
+ *   key = splitmix64(run_seed) ^ (pixel_index << 20) ^ sample_index
+ *   v   = splitmix64(key)
  * pixel_index = y * width + x over the WHOLE frame, so a pixel's samples are
- * identical no matter which GPU / tile / pass renders them.
+ * identical no matter which GPU / tile / pass renders them.  Every stream is
+ * a window of the reference's one sequence, at a hashed 64-bit offset.
  *
- * Why PCG and not xoroshiro: the GPU evaluates a scatter loop's rejection
- * attempts 64 at a time (one attempt per lane) and must know the engine state
- * 3*l draws ahead for lane l.  An LCG core jumps k steps in O(1):
- *   state_{n+k} = A_k * state_n + G_k * inc,  A_k = M^k,  G_k = sum_{j<k} M^j,
- * while xoroshiro needs a 128x128 GF(2) matrix-vector product per jump.
- * Per-sample increments make every stream a distinct sequence (no overlap).
+ * The GPU evaluates a scatter loop's rejection attempts 64 at a time (one
+ * attempt per lane) and must know the state 3*l draws ahead for lane l; an LCG
+ * jumps k steps in O(1):
+ *   v_{n+k} = A_k * v_n + G_k * c,  A_k = M^k,  G_k = sum_{j<k} M^j.
+ * `inc` (= c) is kept in the engine state so the jump formula is explicit.
  */
 #ifndef PT_ENGINE_H
 #define PT_ENGINE_H
@@ -38,8 +37,8 @@
 #define PT_HD static inline
 #endif
 
-#define PT_PCG_MULT 6364136223846793005ULL
-#define PT_STREAM_SALT 0xD1B54A32D192ED03ULL
+#define PT_LCG_MULT 214013ULL  /* include/path-trace.h:47 */
+#define PT_LCG_INC 2531011ULL  /* include/path-trace.h:47 */
 #define PT_SPLITMIX_GAMMA 0x9E3779B97F4A7C15ULL
 
 PT_HD uint64_t pt_splitmix64(uint64_t x)
@@ -50,12 +49,8 @@ PT_HD uint64_t pt_splitmix64(uint64_t x)
     return z ^ (z >> 31);
 }
 
-PT_HD uint32_t pt_pcg_output(uint64_t old)
-{
-    uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
-    uint32_t rot = (uint32_t)(old >> 59);
-    return (xs >> rot) | (xs << ((32u - rot) & 31u));
-}
+/* DefaultRandomEngine::operator()'s output of the UPDATED state */
+PT_HD uint32_t pt_lcg_output(uint64_t updated) { return (uint32_t)(updated >> 32); }
 
 PT_HD uint64_t pt_sample_key(uint64_t run_seed, uint64_t pixel_index, uint64_t sample_index)
 {
@@ -65,13 +60,13 @@ PT_HD uint64_t pt_sample_key(uint64_t run_seed, uint64_t pixel_index, uint64_t s
 PT_HD void pt_engine_seed(uint64_t key, uint64_t *state, uint64_t *inc)
 {
     *state = pt_splitmix64(key);
-    *inc = (pt_splitmix64(key ^ PT_STREAM_SALT) << 1) | 1ULL;
+    *inc = PT_LCG_INC;
 }
 
 /* (A_k, G_k) of the jump state_{n+k} = A_k*state_n + G_k*inc. */
-PT_HD void pt_pcg_jump_coeffs(uint32_t k, uint64_t *a_out, uint64_t *g_out)
+PT_HD void pt_lcg_jump_coeffs(uint32_t k, uint64_t *a_out, uint64_t *g_out)
 {
-    uint64_t a = 1, g = 0, m = PT_PCG_MULT, h = 1; /* h = sum_{j<2^i} M^j for current power m = M^(2^i) */
+    uint64_t a = 1, g = 0, m = PT_LCG_MULT, h = 1; /* h = sum_{j<2^i} M^j for current power m = M^(2^i) */
     while (k) {
         if (k & 1u) {
             /* apply block of size 2^i: (a, g) <- (m*a, m*g + h) */
@@ -106,16 +101,15 @@ struct PtSampleEngine
     PT_HDM static unsigned max() { return 0xFFFFFFFFu; }
     PT_HDM unsigned operator()()
     {
-        uint64_t old = state;
-        state = old * PT_PCG_MULT + inc;
-        return pt_pcg_output(old);
+        state = state * PT_LCG_MULT + inc;
+        return pt_lcg_output(state);
     }
     PT_HDM void discard(uint64_t k)
     {
         while (k) {
             uint32_t step = k > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)k;
             uint64_t a, g;
-            pt_pcg_jump_coeffs(step, &a, &g);
+            pt_lcg_jump_coeffs(step, &a, &g);
             state = a * state + g * inc;
             k -= step;
         }

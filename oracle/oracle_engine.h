@@ -1,7 +1,8 @@
 /*
  * oracle_engine.h -- TEST INFRASTRUCTURE ONLY.  An independent restatement of
- * the per-(pixel, sample) engine specified in include/pt/pt_engine.h (PCG32
- * XSH-RR with a splitmix64-derived state and odd stream increment), written
+ * the per-(pixel, sample) engine specified in include/pt/pt_engine.h (the
+ * reference DefaultRandomEngine recurrence 214013 v + 2531011, output v >> 32,
+ * from a splitmix64-derived starting state), written
  * separately so that a bug in the product header cannot hide behind a shared
  * implementation.  tests/test_engine.py pins both against a pure-Python model.
  */
@@ -33,21 +34,17 @@ public:
     {
         uint64_t key = splitmix(seed) ^ (pixel << 20) ^ sample;
         s = splitmix(key);
-        inc = (splitmix(key ^ 0xD1B54A32D192ED03ull) << 1) | 1ull;
     }
     static unsigned min() { return 0u; }
     static unsigned max() { return 0xFFFFFFFFu; }
     unsigned operator()()
     {
-        uint64_t x = s;
-        s = x * 6364136223846793005ull + inc;
-        uint32_t v = (uint32_t)((x ^ (x >> 18)) >> 27);
-        uint32_t r = (uint32_t)(x >> 59);
-        return r ? (v >> r) | (v << (32 - r)) : v;
+        s = 214013ull * s + 2531011ull; /* include/path-trace.h:45-49 */
+        return (unsigned)(s >> 32);
     }
     uint64_t draws = 0; /* statistics only */
 private:
-    uint64_t s, inc;
+    uint64_t s;
 };
 
 /* The reference's DefaultRandomEngine restated (include/path-trace.h:21-54):

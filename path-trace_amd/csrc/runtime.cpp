@@ -409,7 +409,7 @@ void load_text(SceneImpl &s, const std::string &text)
 std::vector<uint64_t> jump_table()
 {
     std::vector<uint64_t> t(2 * 193);
-    for (uint32_t m = 0; m <= 192; m++) pt_pcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
+    for (uint32_t m = 0; m <= 192; m++) pt_lcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
     return t;
 }
 

@@ -1,6 +1,7 @@
 """The per-(pixel, sample) engine (include/pt/pt_engine.h) against an
 independent pure-Python model, the oracle, and the reference driver's KAT
-stream; and the O(1) jump the GPU bursts rely on against plain stepping."""
+stream; the model's recurrence against the reference DefaultRandomEngine's own
+outputs; and the O(1) jump the GPU bursts rely on against plain stepping."""
 import os
 import subprocess
 
@@ -10,7 +11,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
 M64 = (1 << 64) - 1
-MULT = 6364136223846793005
+MULT = 214013    # DefaultRandomEngine, reference include/path-trace.h:45-49
+INC = 2531011
 
 
 def splitmix(x):
@@ -21,17 +23,14 @@ def splitmix(x):
 
 
 class PyEngine:
-    def __init__(self, seed, pixel, sample):
+    def __init__(self, seed, pixel, sample, state=None):
         key = splitmix(seed) ^ (pixel << 20) ^ sample
-        self.s = splitmix(key)
-        self.inc = ((splitmix(key ^ 0xD1B54A32D192ED03) << 1) | 1) & M64
+        self.s = splitmix(key) if state is None else state
+        self.inc = INC
 
     def __call__(self):
-        old = self.s
-        self.s = (old * MULT + self.inc) & M64
-        xs = (((old >> 18) ^ old) >> 27) & 0xFFFFFFFF
-        rot = old >> 59
-        return ((xs >> rot) | (xs << ((32 - rot) & 31))) & 0xFFFFFFFF
+        self.s = (self.s * MULT + self.inc) & M64
+        return self.s >> 32
 
 
 def jump(k):
@@ -45,6 +44,16 @@ def test_python_model_matches_reference_driver_stream():
     kat = np.load(os.path.join(GOLD, "kat.npy"))
     e = PyEngine(0x5EED, 7, 3)
     assert [e() for _ in range(16)] == [int(v) for v in kat[15:31]]
+
+
+def test_recurrence_is_the_reference_default_engine():
+    """DefaultRandomEngine seed(0) -> v = 0 ^ 0x12476242 (include/path-trace.h:36-39);
+    its outputs, frozen from the unmodified reference, are the
+    model's outputs from that state."""
+    e = PyEngine(0, 0, 0, state=0 ^ 0x12476242)
+    assert [e() for _ in range(5)] == [15280, 3270311074, 2688171609, 1391346033, 351105505]
+    e = PyEngine(0, 0, 0, state=1 ^ 0x12476242)
+    assert [e() for _ in range(5)] == [15280, 3270311084, 2690453845, 193305694, 806675984]
 
 
 def test_jump_equals_stepping():
@@ -68,11 +77,11 @@ def header_probe(tmp_path_factory):
 #include "pt/pt_engine.h"
 int main(void) {
     for (unsigned k = 0; k <= 200; k++) {
-        uint64_t a, g; pt_pcg_jump_coeffs(k, &a, &g);
+        uint64_t a, g; pt_lcg_jump_coeffs(k, &a, &g);
         printf("%u %llu %llu\n", k, (unsigned long long)a, (unsigned long long)g);
     }
     uint64_t st, inc; pt_engine_seed(pt_sample_key(0x5EED, 7, 3), &st, &inc);
-    for (int i = 0; i < 16; i++) { uint64_t o = st; st = o * PT_PCG_MULT + inc; printf("o %u\n", pt_pcg_output(o)); }
+    for (int i = 0; i < 16; i++) { st = st * PT_LCG_MULT + inc; printf("o %u\n", pt_lcg_output(st)); }
     return 0;
 }''')
     exe = d / "probe"

@@ -421,6 +421,12 @@ struct Sph
         c.omc = univ(o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
         c.c = unif(dot(c.omc, c.omc) - e.P[OFF + 3]);
     }
+    /* the same for a per-lane origin */
+    __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e)
+    {
+        c.omc = o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
+        c.c = dot(c.omc, c.omc) - e.P[OFF + 3];
+    }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &)
     {
         const float b = dot(c.omc, q.d);
@@ -493,6 +499,10 @@ struct Pln
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)
     {
         c.num = unif(-e.P[OFF + 3] - dot(o, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2])));
+    }
+    __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e)
+    {
+        c.num = -e.P[OFF + 3] - dot(o, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)
     {
@@ -570,6 +580,11 @@ struct Pln
     {                                                                                               \
         A::prep(c.a, o, e);                                                                         \
         B::prep(c.b, o, e);                                                                         \
+    }                                                                                               \
+    __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e)                      \
+    {                                                                                               \
+        A::prep_l(c.a, o, e);                                                                       \
+        B::prep_l(c.b, o, e);                                                                       \
     }                                                                                               \
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)   \
     {                                                                                               \
@@ -756,6 +771,7 @@ struct Xf
     };
     typedef typename C::St St;
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e) { C::prep(c.c, univ(m_apply(e.P + MOFF, o)), e); }
+    __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e) { C::prep_l(c.c, m_apply(e.P + MOFF, o), e); }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)
     {
         C::init(s, c.c, mkray(m_lin(e.P + MOFF, q.d)), e);
@@ -1598,6 +1614,70 @@ __device__ __forceinline__ V3 camera_dir(const PtLaunch &lp, int pix, Rng &rng)
     return mk(x * lp.sw, y * lp.sh, -lp.dist);
 }
 
+/* A whole sample evaluated by one lane when its ray tree is the camera query
+ * plus at most one mirror child that is a leaf (sky, background and other
+ * non-scattering first hits).  Same statements as trace_sample's spine
+ * (PH_ENTER / PH_SETUP / PH_LOOP / PH_RETURN) restricted to that shape;
+ * returns false, leaving the sample to the wave, for any other shape.
+ * nq / nsh = queries / shaded hits, for the statistics. */
+template <class S>
+__device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 d, const CamHit &ch, V3 &res, int &nq,
+                                            int &nsh)
+{
+    const V3 z = mk(0, 0, 0), o = mk(0, 0, 0);
+    nq = 1, nsh = 0;
+    if (!ch.hit) {
+        res = (z + mk(0, 0, 0)) / 1.0f;
+        return true;
+    }
+    const V3 hit = o + ch.t * d;
+    const int mat = ref_mat(ch.ref);
+    V3 nn = S::Root::normal(ref_prim(ch.ref), ch.t, o, d, e);
+    if (ch.ref & FLIP)
+        nn = -nn;
+    float ior;
+    V3 n;
+    if (ch.ex) {
+        n = -nn;
+        ior = S::ior(mat, e);
+    } else {
+        n = nn;
+        ior = (float)(1.0 / (double)S::ior(mat, e));
+    }
+    const V3 retval = S::emis(mat, hit, e);
+    const float strength = 1.0f, add = 1.0f;
+    if (depth <= 0) {
+        res = (z + retval) / 1.0f;
+        return true;
+    }
+    nsh = 1;
+    const float rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
+    if (rf > EPS)
+        return false;
+    const float sc = clamp01(S::scat(mat, hit, e));
+    if (sc > EPS)
+        return false;
+    const float N = 1.0f; /* sc <= eps */
+    const V3 rc = S::refl(mat, hit, e);
+    const V3 refl = reflect(d, n);
+    const float factor = 1.0f - (1.0f - dot(refl, n)) * sc;
+    const V3 w = ((add / N) * factor) * rc;
+    const float cs = (((strength / N) * add) * factor) * length(rc);
+    if (!(depth - 1 <= 0 || cs < EPS))
+        return false;
+    nq = 2;
+    typename S::Root::Ctx ctx;
+    S::Root::prep_l(ctx, hit, e);
+    float t2 = 0.0f;
+    u32 ref2 = 0;
+    bool ex2 = false;
+    V3 col = mk(0, 0, 0);
+    if (first_hit<typename S::Root>(ctx, refl, e, t2, ref2, ex2))
+        col = S::emis(ref_mat(ref2), hit + t2 * refl, e);
+    res = (z + (retval + w * col)) / 1.0f;
+    return true;
+}
+
 template <class S, int MAXD, bool STRICT>
 __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, const WaveLds &L,
                                            const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt,
@@ -1794,6 +1874,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         const long long item0 = chunk * CH;
         /* the chunk's camera queries, one per lane */
         CamHit ch = {0, 0.0f, 0u, 0};
+        int ldone = 0, lq = 0, lsh = 0;
+        V3 lres = mk(0, 0, 0);
         if (lane < CH && item0 + lane < lp.n_items) {
             const long long item = item0 + lane;
             const long long slot = item / lp.nsamp;
@@ -1807,8 +1889,16 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             bool ex = false;
             ch.hit = first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
             ch.ex = ex ? 1 : 0;
+            ldone = lane_sample<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
         }
-        V3 mine = mk(0, 0, 0);
+        {
+            /* statistics of the samples finished by their lane */
+            const u64 D = __ballot(ldone), Q2 = __ballot(ldone && lq == 2), SH = __ballot(ldone && lsh);
+            cnt.queries += (u64)(__popcll(D) + __popcll(Q2));
+            cnt.shaded += (u64)__popcll(SH);
+        }
+        const u64 DONE = __ballot(ldone);
+        V3 mine = lres; /* valid where ldone */
         for (int j = 0; j < CH; j++) {
             const long long item = item0 + j;
             if (item >= lp.n_items)
@@ -1816,11 +1906,12 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             const long long slot = item / lp.nsamp;
             const int s = lp.s0 + (int)(item - slot * lp.nsamp);
             const int pix = pixels ? pixels[slot] : (int)slot;
+            if ((DONE >> j) & 1ull)
+                continue;
             PT_T0(tt);
             const CamHit cam = {__builtin_amdgcn_readlane(ch.hit, j), rdlane(ch.t, j),
                                 (u32)__builtin_amdgcn_readlane((int)ch.ref, j), __builtin_amdgcn_readlane(ch.ex, j)};
-            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], L, jump, A3l, G3l,
-                                                 cnt, cam);
+            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], L, jump, A3l, G3l, cnt, cam);
             PT_ACC(cnt, 6, tt);
             if (lane == j)
                 mine = c;
