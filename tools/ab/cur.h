@@ -17,7 +17,7 @@
  *     LDS instead of the reference's recursion (include/path-trace.h:58-165);
  *   - a scatter loop with scatter_coefficient > eps (path-trace.h:138-163) is a
  *     BURST: the wave evaluates 64 rejection attempts at once, lane l jumping
- *     the PCG stream 3*l draws ahead (O(1) LCG jump), ballots accept / fail /
+ *     the engine stream 3*l draws ahead (O(1) LCG jump), ballots accept / fail /
  *     non-leaf masks, replays the reference's sequential consumption rule with
  *     scalar bit arithmetic, queues accepted leaf children in LDS and traces
  *     them 64 at a time, one child per lane;
@@ -42,7 +42,7 @@ namespace ptd
 
 constexpr float EPS = 1e-3f;      /* include/misc.h:7 */
 constexpr float MAXV = 1e20f;     /* include/misc.h:8 */
-constexpr u64 PCG_MULT = 6364136223846793005ull;
+constexpr u64 LCG_MULT = 214013ull; /* DefaultRandomEngine, include/path-trace.h:47 */
 
 /* -------------------------------------------------------------- launch --- */
 struct PtImage
@@ -256,7 +256,8 @@ __device__ __forceinline__ V3 m_lin(const float *__restrict__ m, V3 v)
 }
 
 /* ----------------------------------------------------------------- rng --- */
-/* PCG32 per (pixel, sample) -- include/pt/pt_engine.h is the specification. */
+/* The reference's DefaultRandomEngine recurrence with a per-(pixel, sample)
+ * starting state -- include/pt/pt_engine.h is the specification. */
 struct Rng
 {
     u64 st, inc;
@@ -268,30 +269,24 @@ __device__ __forceinline__ u64 splitmix64(u64 x)
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ u32 pcg_out(u64 old)
-{
-    u32 xs = (u32)(((old >> 18) ^ old) >> 27);
-    u32 rot = (u32)(old >> 59);
-    return (xs >> rot) | (xs << ((32u - rot) & 31u));
-}
+__device__ __forceinline__ u32 lcg_out(u64 updated) { return (u32)(updated >> 32); }
 __device__ __forceinline__ void rng_seed(Rng &r, u64 seed, u64 pixel, u64 sample)
 {
     u64 key = splitmix64(seed) ^ (pixel << 20) ^ sample;
     r.st = splitmix64(key);
-    r.inc = (splitmix64(key ^ 0xD1B54A32D192ED03ull) << 1) | 1ull;
+    r.inc = 2531011ull;
 }
 __device__ __forceinline__ u32 rng_next(Rng &r)
 {
-    u64 old = r.st;
-    r.st = old * PCG_MULT + r.inc;
-    return pcg_out(old);
+    r.st = r.st * LCG_MULT + r.inc;
+    return lcg_out(r.st);
 }
 /* uniform_real_distribution<float>, vector3d.h:22-33, for (0,1) and (-1,1) */
 __device__ __forceinline__ float u01(u32 o) { return (float)o / 4294967296.0f; }
 /* uniform(-1, 1): (float)o / 2^32 * (1 - -1) + -1 (include/vector3d.h:14-34).
  * Both power-of-two scalings are exact for o >= 1 (and 0 stays 0), so one
  * multiply by 2^-31 gives the same bits. */
-__device__ __forceinline__ float u11(u32 o) { return (float)o * 0x1p-31f + -1.0f; }
+__device__ __forceinline__ float u11(u32 o) { return __builtin_fmaf((float)o, 0x1p-31f, -1.0f); } /* exact product: == mul then add */
 
 /* --------------------------------------------------------- wave helpers --- */
 __device__ __forceinline__ float rdlane(float v, int l)
@@ -1135,7 +1130,7 @@ static_assert(64 + 64 * PT_KATT <= PT_QCAP, "queue too small for PT_KATT");
 #define PT_JUMP_ENTRIES 193 /* host table: m = 0..192 attempts (PT_KATT <= 3) */
 
 /* One rejection attempt of the scatter loop body (path-trace.h:141-158):
- * draws s0, s1, s2 are the attempt's three engine states. */
+ * s0 is the engine state before the attempt's three draws (outputs of s1, s2, s3). */
 struct Attempt
 {
     V3 wn;        /* accepted direction (unnormalised in deferred mode)      */
@@ -1149,9 +1144,10 @@ template <bool DEFERRED, bool KR0>
 __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float sc, float sNa, float abs_rc,
                                            bool child_leaf_depth)
 {
-    const u64 s1 = s0 * PCG_MULT + inc;
-    const u64 s2 = s1 * PCG_MULT + inc;
-    const V3 v = mk(u11(pcg_out(s0)), u11(pcg_out(s1)), u11(pcg_out(s2)));
+    const u64 s1 = s0 * LCG_MULT + inc;
+    const u64 s2 = s1 * LCG_MULT + inc;
+    const u64 s3 = s2 * LCG_MULT + inc;
+    const V3 v = mk(u11(lcg_out(s1)), u11(lcg_out(s2)), u11(lcg_out(s3)));
     /* rand(): while (mag > max) with mag = sqrt(|v|^2); correctly rounded
      * sqrt(x) > 1  <=>  x > 1 + 2^-23 (exhaustively checked) */
     const bool ball = !(dot(v, v) > 0x1.000002p+0f);
