@@ -1095,7 +1095,7 @@ struct Counters
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
-    float4 *q;            /* PT_QCAP queued leaf-child rays (direction, factor)           */
+    V3 *q;                /* PT_QCAP queued leaf-child directions                         */
     void *ctx;            /* the burst origin's S::Root::Ctx, prepared once per burst     */
     float4 *ring;         /* PT_RCAP kept-child slots: parked ray, then the child's term */
     u64 *gmask;           /* PT_GCAP groups of 64 children: which lanes hold a ring slot */
@@ -1127,14 +1127,15 @@ struct Frame
 enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 
 #ifndef PT_KATT
-#define PT_KATT 2 /* rejection attempts per lane per generation round */
+#define PT_KATT 4 /* rejection attempts per lane per generation round */
 #endif
 #define PT_QCAP (64 + 64 * PT_KATT) /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
 #define PT_RCAP 256 /* kept-child slots per wave awaiting their group sum          */
 #define PT_GCAP 32  /* groups per wave awaiting their sum                           */
 #define PT_SCAP 256 /* parked children per queue (byte offsets): a drain can add 2 x 64 to < 64 */
 static_assert(64 + 64 * PT_KATT <= PT_QCAP, "queue too small for PT_KATT");
-#define PT_JUMP_ENTRIES 193 /* host table: m = 0..192 attempts (PT_KATT <= 3) */
+#define PT_JUMP_ENTRIES 321 /* host table: m = 0..320 attempts */
+static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
 
 /* One rejection attempt of the scatter loop body (path-trace.h:141-158):
  * s0 is the engine state before the attempt's three draws (outputs of s1, s2, s3). */
@@ -1253,7 +1254,8 @@ template <class S, bool STRICT, bool DEFERRED, bool KR0>
 __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
-    float4 *const q = L.q, *const ring = L.ring;
+    V3 *const q = L.q;
+    float4 *const ring = L.ring;
     unsigned char *const fastq = L.fastq, *const slowq = L.slowq;
     const int lane = threadIdx.x & 63;
     const u64 below = (1ull << lane) - 1ull;
@@ -1352,8 +1354,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
                 if ((take[k] >> lane) & 1ull)
-                    q[qwrap(base + __popcll(take[k] & below))] =
-                        make_float4(at[k].wn.x, at[k].wn.y, at[k].wn.z, at[k].factor);
+                    q[qwrap(base + __popcll(take[k] & below))] = at[k].wn;
                 base = qwrap(base + __popcll(take[k]));
                 qn += __popcll(take[k]);
             }
@@ -1377,12 +1378,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             int lit = 0, keep = 0;
             float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             if (lane < cntb) {
-                float4 en = q[qwrap(qhead + lane)];
-                V3 dir = mk(en.x, en.y, en.z);
-                if (DEFERRED) {
+                V3 dir = q[qwrap(qhead + lane)];
+                if (DEFERRED)
                     dir = cnormalize(dir);
-                    en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
-                }
+                /* the factor of path-trace.h:160, the same expression as at
+                 * generation in the non-deferred case */
+                float4 en;
+                en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
 #if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
                 /* experiment: generation cost only */
                 {
@@ -1858,7 +1860,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                                              const PtLaunch &lp)
 {
     __shared__ Frame stk[PT_WPW][MAXD + 1];
-    __shared__ float4 qbuf[PT_WPW][PT_QCAP];
+    __shared__ V3 qbuf[PT_WPW][PT_QCAP];
     __shared__ typename S::Root::Ctx xbuf[PT_WPW];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
     __shared__ u64 gbuf[PT_WPW][PT_GCAP];

@@ -1077,6 +1077,12 @@ struct Counters
 #define PT_CNT(c, k, v)
 #endif
 };
+/* ISA markers for static instruction counts (tools/isa_sections.py) */
+#ifdef PT_MARKERS
+#define PT_MARK(n) asm volatile("s_nop " #n)
+#else
+#define PT_MARK(n)
+#endif
 /* Per-phase wave cycle counters (profiling builds only: PT_DEVICE_DEFINES="PT_PHASE_TIMING") */
 #ifdef PT_PHASE_TIMING
 #define PT_T0(v) const u64 v = __builtin_amdgcn_s_memtime()
@@ -1090,6 +1096,7 @@ struct Counters
 struct WaveLds
 {
     float4 *q;            /* PT_QCAP queued leaf-child rays (direction, factor)           */
+    void *ctx;            /* the burst origin's S::Root::Ctx, prepared once per burst     */
     float4 *ring;         /* PT_RCAP kept-child slots: parked ray, then the child's term */
     u64 *gmask;           /* PT_GCAP groups of 64 children: which lanes hold a ring slot */
     unsigned char *fastq; /* PT_SCAP slots waiting for the fast pass (position mod 256) */
@@ -1122,7 +1129,7 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #ifndef PT_KATT
 #define PT_KATT 2 /* rejection attempts per lane per generation round */
 #endif
-#define PT_QCAP 256 /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
+#define PT_QCAP (64 + 64 * PT_KATT) /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
 #define PT_RCAP 256 /* kept-child slots per wave awaiting their group sum          */
 #define PT_GCAP 32  /* groups per wave awaiting their sum                           */
 #define PT_SCAP 256 /* parked children per queue (byte offsets): a drain can add 2 x 64 to < 64 */
@@ -1264,6 +1271,15 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const u64 A64 = jump[128], g64inc = jump[129] * rng.inc;   /* 64 attempts = 192 draws  */
     const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * rng.inc; /* a full round */
     int qhead = 0, qn = 0, fails = 0, reason = -1;
+    /* x mod PT_QCAP for 0 <= x < 2 * PT_QCAP */
+    auto qwrap = [](int x) { return (int)min((u32)x, (u32)(x - PT_QCAP)); };
+    /* the burst origin's primitive contexts, shared by every pass of the burst */
+    typename S::Root::Ctx *const cxp = (typename S::Root::Ctx *)L.ctx;
+    {
+        typename S::Root::Ctx c;
+        S::Root::prep(c, hit, e);
+        *cxp = c;
+    }
     /* children are numbered in stage-A order (npos); stage A's batches of 64 are
      * the summation groups.  A DARK child (no emissive primitive reachable, and a
      * positive weight) has the burst-uniform term Z = rc * 0 and takes no ring
@@ -1332,15 +1348,15 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 child.depth = depth - 1;
             }
             n_att += (u32)m;
-            int base = qhead + qn;
+            int base = qwrap(qhead + qn);
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
                 if ((take[k] >> lane) & 1ull)
-                    q[(base + __popcll(take[k] & below)) & (PT_QCAP - 1)] =
+                    q[qwrap(base + __popcll(take[k] & below))] =
                         make_float4(at[k].wn.x, at[k].wn.y, at[k].wn.z, at[k].factor);
-                base += __popcll(take[k]);
+                base = qwrap(base + __popcll(take[k]));
+                qn += __popcll(take[k]);
             }
-            qn = base - qhead;
             /* ---- advance the sample's stream past the consumed attempts */
             if (m == 64 * PT_KATT)
                 rng.st = Afull * rng.st + gfullinc;
@@ -1361,7 +1377,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             int lit = 0, keep = 0;
             float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             if (lane < cntb) {
-                float4 en = q[(qhead + lane) & (PT_QCAP - 1)];
+                float4 en = q[qwrap(qhead + lane)];
                 V3 dir = mk(en.x, en.y, en.z);
                 if (DEFERRED) {
                     dir = cnormalize(dir);
@@ -1377,8 +1393,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 }
 #else
                 {
-                    typename S::Root::Ctx ctx;
-                    S::Root::prep(ctx, hit, e);
+                    const typename S::Root::Ctx ctx = *cxp;
                     PrimSpans<S::Root::HI> ps;
                     S::Root::template span_sel<Emissive<S>>(ps, ctx, mkray(dir), e);
                     S::Root::template each_sel<Emissive<S>>([&](auto x) {
@@ -1415,7 +1430,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             n_dark += (u32)(cntb - __popcll(LM));
             npos += cntb;
             n_leaf += (u32)cntb;
-            qhead += cntb;
+            qhead = qwrap(qhead + cntb);
             qn -= cntb;
             i += cntb;
             PT_ACC(cnt, 1, ta);
@@ -1442,16 +1457,21 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
                 const float4 en = ring[pos & (PT_RCAP - 1)];
                 const V3 dir = mk(en.x, en.y, en.z);
-                typename S::Root::Ctx ctx;
-                S::Root::prep(ctx, hit, e);
+                PT_MARK(8);
+                const typename S::Root::Ctx ctx = *cxp;
                 PrimSpans<S::Root::HI> ps;
+                PT_MARK(9);
                 S::Root::span(ps, ctx, mkray(dir), e);
-                if (S::Root::fast_ok(ps)) {
+                PT_MARK(10);
+                const int fok = S::Root::fast_ok(ps);
+                PT_MARK(11);
+                if (fok) {
                     float t = 0.0f;
                     int mat = 0;
                     V3 col = mk(0, 0, 0);
                     if (fast_first_hit<typename S::Root>(ps, t, mat))
                         col = S::emis(mat, hit + t * dir, e);
+                    PT_MARK(12);
                     const V3 term = ((aN * en.w) * rc) * col;
                     ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
                 } else {
@@ -1490,8 +1510,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 const int pos = slot_pos(slowq[(s_head + lane) & (PT_SCAP - 1)]);
                 const float4 en = ring[pos & (PT_RCAP - 1)];
                 const V3 dir = mk(en.x, en.y, en.z);
-                typename S::Root::Ctx ctx;
-                S::Root::prep(ctx, hit, e);
+                const typename S::Root::Ctx ctx = *cxp;
                 float t;
                 u32 ref;
                 bool ex;
@@ -1840,6 +1859,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
 {
     __shared__ Frame stk[PT_WPW][MAXD + 1];
     __shared__ float4 qbuf[PT_WPW][PT_QCAP];
+    __shared__ typename S::Root::Ctx xbuf[PT_WPW];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
     __shared__ u64 gbuf[PT_WPW][PT_GCAP];
     __shared__ unsigned char fbuf[PT_WPW][PT_SCAP];
@@ -1856,7 +1876,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
 #endif
-    const WaveLds L = {qbuf[wave], rbuf[wave], gbuf[wave], fbuf[wave], sbuf[wave]};
+    const WaveLds L = {qbuf[wave], &xbuf[wave], rbuf[wave], gbuf[wave], fbuf[wave], sbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */

@@ -1,4 +1,5 @@
-R"PTDEV(/*
+#define PT_KATT 4
+/*
  * pt_device.h -- CDNA4 (gfx950) device library of the MI355X path tracer.
  *
  * Embedded verbatim into every scene module that the runtime generates and
@@ -1127,7 +1128,7 @@ struct Frame
 enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 
 #ifndef PT_KATT
-#define PT_KATT 4 /* rejection attempts per lane per generation round */
+#define PT_KATT 2 /* rejection attempts per lane per generation round */
 #endif
 #define PT_QCAP (64 + 64 * PT_KATT) /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
 #define PT_RCAP 256 /* kept-child slots per wave awaiting their group sum          */
@@ -2063,4 +2064,3 @@ extern "C" __global__ void pt_selftest_math(u64 n, u64 seed, unsigned long long 
         atomicAdd(&bad[2], bn);
 }
 #endif
-)PTDEV"
