@@ -313,14 +313,26 @@ __device__ __forceinline__ float dpp_partner(float v)
 {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+/* v + src broadcast from the last lane of the row(s) below, on rows ROWS only;
+ * the other rows add -0.0f, which leaves every value (and the sign of 0) */
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_bcast_add(float v)
+{
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-0.0f), __float_as_int(v), CTRL, ROWS, 0xF,
+                                                          false));
+}
 __device__ __forceinline__ float wave_tree_sum(float v)
 {
     v = v + dpp_partner<0xB1>(v);  /* quad_perm [1,0,3,2]: lane ^ 1 */
     v = v + dpp_partner<0x4E>(v);  /* quad_perm [2,3,0,1]: lane ^ 2 */
     v = v + dpp_partner<0x141>(v); /* row_half_mirror: partner in the other quad of the 8 */
     v = v + dpp_partner<0x140>(v); /* row_mirror: partner in the other 8 of the row */
-    float r0 = rdlane(v, 0), r1 = rdlane(v, 16), r2 = rdlane(v, 32), r3 = rdlane(v, 48);
-    return (r0 + r1) + (r2 + r3);
+    /* rows now hold r0..r3 in every lane; row_bcast:15 gives rows 1 and 3
+     * r1 + r0 and r3 + r2, row_bcast:31 gives row 3 (r3 + r2) + (r1 + r0):
+     * by commutativity the bits of (r0 + r1) + (r2 + r3) */
+    v = dpp_bcast_add<0x142, 0xA>(v);
+    v = dpp_bcast_add<0x143, 0x8>(v);
+    return rdlane(v, 63);
 }
 
 /* ----------------------------------------------------------- CSG spans --- */
