@@ -487,6 +487,28 @@ struct Sph
     {
         return normalize((o + t * d) - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
+    /* Sound test on an UNNORMALISED direction w that the span of normalize(w)
+     * is dead or ends before EPS (stage A of the scatter loop).  Origin
+     * outside (c > 0) and receding (b > 0): disc = fl(fl(b*b) - a*c) <= fl(b*b),
+     * so sqrt(disc) <= b and t1 = (-b + sqrt(disc)) / a <= 0.  b's sign is
+     * read off B = omc.w with a margin (1e-6 of sum |omc_i w_i|) that covers
+     * the rounding of normalize() and of both dot products. */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return true; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &)
+    {
+        if constexpr (!SEL::take(MAT))
+            return true;
+        const float B = dot(c.omc, w);
+        const float s = (__builtin_fabsf(c.omc.x * w.x) + __builtin_fabsf(c.omc.y * w.y)) +
+                        __builtin_fabsf(c.omc.z * w.z);
+        const bool pre = c.c > 0.0f && (__builtin_fabsf(c.omc.x) + __builtin_fabsf(c.omc.y)) +
+                                               __builtin_fabsf(c.omc.z) < 1e15f;
+        return pre && B > __builtin_fmaxf(1e-6f * s, 1e-30f);
+    }
 };
 
 /* Plane half-space {p : n.p + d < 0} (src/plane.cpp:35-63).  P[OFF..] = n, d. */
@@ -564,6 +586,26 @@ struct Pln
     {
         return normalize(mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
+    /* Sound dark test on an unnormalised direction w (see Sph::dark_raw).
+     * With num <= -1e-6 the span of normalize(w) is dead or ends before EPS
+     * unless div = n.normalize(w) <= -1e-6: div in (-1e-6, 1e-6) is
+     * degenerate (dead), div >= 1e-6 gives t1 = num / div < 0 (or |t| >= 1e20,
+     * dead).  For |n|_1 <= 1.5 the computed div lies within 6.1e-7 |n|_1 <
+     * 1e-6 of (n.w) / |w| for a computed n.w >= 0, so n.w >= 0 suffices. */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return true; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &e)
+    {
+        if constexpr (!SEL::take(MAT))
+            return true;
+        const V3 np = mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
+        const bool pre = c.num <= -(EPS * EPS) &&
+                         (__builtin_fabsf(np.x) + __builtin_fabsf(np.y)) + __builtin_fabsf(np.z) <= 1.5f;
+        return pre && dot(w, np) >= 0.0f;
+    }
 };
 
 /* Binary CSG nodes: pull-protocol restatement of the reference iterators.
@@ -630,6 +672,15 @@ struct Pln
         if (prim < A::HI)                                                                           \
             return A::normal(prim, t, o, d, e);                                                     \
         return B::normal(prim, t, o, d, e);                                                         \
+    }                                                                                               \
+    template <class SEL>                                                                            \
+    __device__ static constexpr bool raw_ok() { return A::template raw_ok<SEL>() && B::template raw_ok<SEL>(); } \
+    template <class SEL>                                                                            \
+    __device__ static constexpr int nsel() { return A::template nsel<SEL>() + B::template nsel<SEL>(); } \
+    template <class SEL>                                                                            \
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &e)              \
+    {                                                                                               \
+        return A::template dark_raw<SEL>(c.a, w, e) & B::template dark_raw<SEL>(c.b, w, e);         \
     }
 
 /* Each merge step decides what to emit and which child to advance, then
@@ -805,6 +856,13 @@ struct Xf
         V3 n = C::normal(prim, t, m_apply(e.P + MOFF, o), m_lin(e.P + MOFF, d), e);
         return normalize(m_lin(e.P + IOFF, n));
     }
+    /* no raw-direction dark test through a transform unless nothing inside is selected */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return C::template nsel<SEL>() == 0; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return C::template nsel<SEL>(); }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &, V3, const Env &) { return true; }
 };
 
 /* First qualifying span of the root, traceRay's scan (path-trace.h:66-100). */
@@ -1309,6 +1367,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     /* ((aN * factor) * rc) * (+0) == rc * (+0) bitwise for any finite aN * factor > 0 */
     const V3 Z = rc * mk(0.0f, 0.0f, 0.0f);
     int fast_on = 1;
+    /* RAW: stage A decides dark children on the unnormalised direction
+     * (dark_raw, sound but conservative).  Its Z shortcut also needs a factor
+     * >= +0, i.e. a computed dot(normalize(w), n) >= 0: accepted w have a
+     * computed n.w > EPS and |w| <= 1 + |kR| (< 65), so the rounding of
+     * normalize and dot (< 7e-5 here) cannot flip the sign. */
+    constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
+    const bool raw_on = KR0 || length(kR) < 64.0f;
     u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
     PT_CNT(cnt, 0, 1);
     for (;;) {
@@ -1389,7 +1454,18 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             PT_CNT(cnt, 2, 1);
             int lit = 0, keep = 0;
             float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (lane < cntb) {
+            if (RAW) {
+                /* every child here is a leaf: the raw test alone decides dark;
+                 * kept children park their unnormalised direction and the fast
+                 * pass normalises them, 64 useful lanes at a time */
+                if (lane < cntb) {
+                    const V3 w = q[qwrap(qhead + lane)];
+                    const typename S::Root::Ctx ctx = *cxp;
+                    keep = !(raw_on && S::Root::template dark_raw<Emissive<S>>(ctx, w, e));
+                    lit = keep;
+                    out = make_float4(w.x, w.y, w.z, 0.0f);
+                }
+            } else if (lane < cntb) {
                 V3 dir = q[qwrap(qhead + lane)];
                 if (DEFERRED)
                     dir = cnormalize(dir);
@@ -1467,9 +1543,20 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 /* the fast check keeps failing in this burst: park for the full merge */
                 pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
                 slow = 1;
+                if (RAW) {
+                    const float4 en = ring[pos & (PT_RCAP - 1)];
+                    const V3 dir = cnormalize(mk(en.x, en.y, en.z));
+                    ring[pos & (PT_RCAP - 1)] = make_float4(dir.x, dir.y, dir.z, 1.0f - (1.0f - dot(dir, n)) * sc);
+                }
             } else if (lane < cf) {
                 pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
-                const float4 en = ring[pos & (PT_RCAP - 1)];
+                float4 en = ring[pos & (PT_RCAP - 1)];
+                if (RAW) {
+                    /* the normalisation and factor stage A left to this pass
+                     * (the same expressions as path-trace.h:157, :160) */
+                    const V3 nd = cnormalize(mk(en.x, en.y, en.z));
+                    en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
+                }
                 const V3 dir = mk(en.x, en.y, en.z);
                 PT_MARK(8);
                 const typename S::Root::Ctx ctx = *cxp;
@@ -1494,6 +1581,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     ring[pos & (PT_RCAP - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #else
                     slow = 1;
+                    if (RAW)
+                        ring[pos & (PT_RCAP - 1)] = en;
 #endif
                 }
             }
