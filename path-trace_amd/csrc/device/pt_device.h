@@ -1380,6 +1380,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
         PT_CNT(cnt, 1, 1);
         if (reason < 0 && qn < 64) {
             PT_T0(tg);
+            PT_MARK(13);
             /* ---- generation round: lane l evaluates attempts l, 64 + l, ... */
             Attempt at[PT_KATT];
             u64 Am[PT_KATT], Fm[PT_KATT], NLm[PT_KATT];
@@ -1441,9 +1442,11 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             else
                 rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
             PT_ACC(cnt, 0, tg);
+            PT_MARK(15);
         }
         if (qn >= 64 || (reason >= 0 && qn > 0)) {
             PT_T0(ta);
+            PT_MARK(14);
             /* ---- stage A: one queued leaf child per lane.  A child whose ray no
              * emissive primitive meets at t >= eps has the term weight * (+0)
              * whatever the CSG makes of it (merges only copy primitive
@@ -1524,6 +1527,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             qn -= cntb;
             i += cntb;
             PT_ACC(cnt, 1, ta);
+            PT_MARK(15);
         }
         const bool final = reason >= 0 && qn == 0;
         /* queued slots hold ring numbers mod 256; every pending one lies in
@@ -1655,6 +1659,36 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 if ((gm >> lane) & 1ull) {
                     const float4 tv = ring[(keep_sum + __popcll(gm & below)) & (PT_RCAP - 1)];
                     term = mk(tv.x, tv.y, tv.z);
+                }
+                if (!STRICT && gsum + 1 < ngrp) {
+                    /* groups finish in batches (a slow pass resolves many at
+                     * once): when the next group is finished too, its six
+                     * tree sums run interleaved with these; retval still adds
+                     * the group sums one after the other */
+                    const u64 gm2 = ((u64)(u32)uni((int)(nx >> 32)) << 32) | (u64)(u32)uni((int)nx);
+                    const int gk2 = __popcll(gm2);
+                    if (keep_sum + gk + gk2 <= resolved) {
+                        u64 nx2 = 0ull;
+                        if (gsum + 2 < ngrp)
+                            nx2 = gmask[(gsum + 2) & (PT_GCAP - 1)];
+                        const int cg2 = min(64, npos - 64 * (gsum + 1));
+                        PT_CNT(cnt, 5, 1);
+                        V3 term2 = mk(-0.0f, -0.0f, -0.0f);
+                        if (lane < cg2)
+                            term2 = Z;
+                        if ((gm2 >> lane) & 1ull) {
+                            const float4 tv = ring[(keep_sum + gk + __popcll(gm2 & below)) & (PT_RCAP - 1)];
+                            term2 = mk(tv.x, tv.y, tv.z);
+                        }
+                        const V3 g1 = mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
+                        const V3 g2 = mk(wave_tree_sum(term2.x), wave_tree_sum(term2.y), wave_tree_sum(term2.z));
+                        retval = univ(retval + g1);
+                        retval = univ(retval + g2);
+                        keep_sum += gk + gk2;
+                        gsum += 2;
+                        head_gm = ((u64)(u32)uni((int)(nx2 >> 32)) << 32) | (u64)(u32)uni((int)nx2);
+                        continue;
+                    }
                 }
                 if (STRICT) {
                     for (int j = 0; j < cg; j++)
