@@ -405,6 +405,22 @@ __device__ __forceinline__ int sep(const PS &ps, int x, int y)
     return (!ps.live[x]) | (!ps.live[y]) | (ps.t1[x] < ps.t0[y]) | (ps.t1[y] < ps.t0[x]) |
            ((ps.t1[x] < EPS) & (ps.t1[y] < EPS));
 }
+/* At a Union node (src/union.cpp:84-134) overlapping spans merge into one
+ * whose start is the earlier start (the B side's on a tie, :125-132); when
+ * both starts are >= EPS and differ, that merged span begins at the smaller
+ * start >= EPS, so traceRay's scan stops at it exactly as at the earlier
+ * span alone -- what fast_first_hit picks.  (A third span separated from both
+ * lies wholly before or after their merge.)  Such pairs pass too: unions of
+ * overlapping half-spaces (C2/C5's sky box, ground planes) stay on the fast
+ * pass.  Difference and Intersection nodes keep the strict rule. */
+template <bool UNION, class PS>
+__device__ __forceinline__ int pair_ok(const PS &ps, int x, int y)
+{
+    int ok = sep(ps, x, y);
+    if (UNION)
+        ok |= (ps.t0[x] >= EPS) & (ps.t0[y] >= EPS) & (ps.t0[x] != ps.t0[y]);
+    return ok;
+}
 
 /* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r.  Branch-free:
  * t0/t1 are computed on every lane (dead lanes' values are never read), with
@@ -664,7 +680,7 @@ struct Pln
     __device__ static __forceinline__ int fast_ok(const PS &ps)                                     \
     {                                                                                               \
         int ok = A::fast_ok(ps) & B::fast_ok(ps);                                                   \
-        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= sep(ps, decltype(x)::value, decltype(y)::value); }); }); \
+        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= pair_ok<IS_UNION>(ps, decltype(x)::value, decltype(y)::value); }); }); \
         return ok;                                                                                  \
     }                                                                                               \
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)       \
@@ -691,6 +707,7 @@ struct Pln
 template <class A, class B>
 struct Uni
 {
+    static constexpr bool IS_UNION = true;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f)
@@ -735,6 +752,7 @@ struct Uni
 template <class A, class B>
 struct Isect
 {
+    static constexpr bool IS_UNION = false;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&) {}
@@ -775,6 +793,7 @@ struct Isect
 template <class A, class B>
 struct Diff
 {
+    static constexpr bool IS_UNION = false;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { A::each_pos(f); }

@@ -17,7 +17,7 @@
  *     LDS instead of the reference's recursion (include/path-trace.h:58-165);
  *   - a scatter loop with scatter_coefficient > eps (path-trace.h:138-163) is a
  *     BURST: the wave evaluates 64 rejection attempts at once, lane l jumping
- *     the PCG stream 3*l draws ahead (O(1) LCG jump), ballots accept / fail /
+ *     the engine stream 3*l draws ahead (O(1) LCG jump), ballots accept / fail /
  *     non-leaf masks, replays the reference's sequential consumption rule with
  *     scalar bit arithmetic, queues accepted leaf children in LDS and traces
  *     them 64 at a time, one child per lane;
@@ -42,7 +42,7 @@ namespace ptd
 
 constexpr float EPS = 1e-3f;      /* include/misc.h:7 */
 constexpr float MAXV = 1e20f;     /* include/misc.h:8 */
-constexpr u64 PCG_MULT = 6364136223846793005ull;
+constexpr u64 LCG_MULT = 214013ull; /* DefaultRandomEngine, include/path-trace.h:47 */
 
 /* -------------------------------------------------------------- launch --- */
 struct PtImage
@@ -256,7 +256,8 @@ __device__ __forceinline__ V3 m_lin(const float *__restrict__ m, V3 v)
 }
 
 /* ----------------------------------------------------------------- rng --- */
-/* PCG32 per (pixel, sample) -- include/pt/pt_engine.h is the specification. */
+/* The reference's DefaultRandomEngine recurrence with a per-(pixel, sample)
+ * starting state -- include/pt/pt_engine.h is the specification. */
 struct Rng
 {
     u64 st, inc;
@@ -268,30 +269,24 @@ __device__ __forceinline__ u64 splitmix64(u64 x)
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ u32 pcg_out(u64 old)
-{
-    u32 xs = (u32)(((old >> 18) ^ old) >> 27);
-    u32 rot = (u32)(old >> 59);
-    return (xs >> rot) | (xs << ((32u - rot) & 31u));
-}
+__device__ __forceinline__ u32 lcg_out(u64 updated) { return (u32)(updated >> 32); }
 __device__ __forceinline__ void rng_seed(Rng &r, u64 seed, u64 pixel, u64 sample)
 {
     u64 key = splitmix64(seed) ^ (pixel << 20) ^ sample;
     r.st = splitmix64(key);
-    r.inc = (splitmix64(key ^ 0xD1B54A32D192ED03ull) << 1) | 1ull;
+    r.inc = 2531011ull;
 }
 __device__ __forceinline__ u32 rng_next(Rng &r)
 {
-    u64 old = r.st;
-    r.st = old * PCG_MULT + r.inc;
-    return pcg_out(old);
+    r.st = r.st * LCG_MULT + r.inc;
+    return lcg_out(r.st);
 }
 /* uniform_real_distribution<float>, vector3d.h:22-33, for (0,1) and (-1,1) */
 __device__ __forceinline__ float u01(u32 o) { return (float)o / 4294967296.0f; }
 /* uniform(-1, 1): (float)o / 2^32 * (1 - -1) + -1 (include/vector3d.h:14-34).
  * Both power-of-two scalings are exact for o >= 1 (and 0 stays 0), so one
  * multiply by 2^-31 gives the same bits. */
-__device__ __forceinline__ float u11(u32 o) { return (float)o * 0x1p-31f + -1.0f; }
+__device__ __forceinline__ float u11(u32 o) { return __builtin_fmaf((float)o, 0x1p-31f, -1.0f); } /* exact product: == mul then add */
 
 /* --------------------------------------------------------- wave helpers --- */
 __device__ __forceinline__ float rdlane(float v, int l)
@@ -318,14 +313,26 @@ __device__ __forceinline__ float dpp_partner(float v)
 {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+/* v + src broadcast from the last lane of the row(s) below, on rows ROWS only;
+ * the other rows add -0.0f, which leaves every value (and the sign of 0) */
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_bcast_add(float v)
+{
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-0.0f), __float_as_int(v), CTRL, ROWS, 0xF,
+                                                          false));
+}
 __device__ __forceinline__ float wave_tree_sum(float v)
 {
     v = v + dpp_partner<0xB1>(v);  /* quad_perm [1,0,3,2]: lane ^ 1 */
     v = v + dpp_partner<0x4E>(v);  /* quad_perm [2,3,0,1]: lane ^ 2 */
     v = v + dpp_partner<0x141>(v); /* row_half_mirror: partner in the other quad of the 8 */
     v = v + dpp_partner<0x140>(v); /* row_mirror: partner in the other 8 of the row */
-    float r0 = rdlane(v, 0), r1 = rdlane(v, 16), r2 = rdlane(v, 32), r3 = rdlane(v, 48);
-    return (r0 + r1) + (r2 + r3);
+    /* rows now hold r0..r3 in every lane; row_bcast:15 gives rows 1 and 3
+     * r1 + r0 and r3 + r2, row_bcast:31 gives row 3 (r3 + r2) + (r1 + r0):
+     * by commutativity the bits of (r0 + r1) + (r2 + r3) */
+    v = dpp_bcast_add<0x142, 0xA>(v);
+    v = dpp_bcast_add<0x143, 0x8>(v);
+    return rdlane(v, 63);
 }
 
 /* ----------------------------------------------------------- CSG spans --- */
@@ -421,11 +428,24 @@ struct Sph
         c.omc = univ(o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
         c.c = unif(dot(c.omc, c.omc) - e.P[OFF + 3]);
     }
+    /* the same for a per-lane origin */
+    __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e)
+    {
+        c.omc = o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
+        c.c = dot(c.omc, c.omc) - e.P[OFF + 3];
+    }
+    template <bool SKIP = false>
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &)
     {
         const float b = dot(c.omc, q.d);
         const float disc = b * b - q.a * c.c;
         const bool live = !(disc <= EPS);
+        if (SKIP && !wave_any(live)) {
+            /* the whole wave misses: skip the roots (dead lanes' t are never read) */
+            s.live = 0;
+            s.t0 = s.t1 = 0.0f;
+            return;
+        }
         const float sq = sqrt_core(disc); /* exact: disc > EPS (or inf/NaN) where live */
         const float n0 = -b - sq, n1 = -b + sq;
         float t0 = div_core(n0, q.ra), t1 = div_core(n1, q.ra);
@@ -450,7 +470,7 @@ struct Sph
     __device__ static __forceinline__ void span(PS &ps, const Ctx &c, const Ray &q, const Env &e)
     {
         St s;
-        init(s, c, q, e);
+        init<true>(s, c, q, e);
         ps.t0[PRIM] = s.t0, ps.t1[PRIM] = s.t1, ps.live[PRIM] = s.live;
     }
     template <class F>
@@ -474,6 +494,28 @@ struct Sph
     {
         return normalize((o + t * d) - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
+    /* Sound test on an UNNORMALISED direction w that the span of normalize(w)
+     * is dead or ends before EPS (stage A of the scatter loop).  Origin
+     * outside (c > 0) and receding (b > 0): disc = fl(fl(b*b) - a*c) <= fl(b*b),
+     * so sqrt(disc) <= b and t1 = (-b + sqrt(disc)) / a <= 0.  b's sign is
+     * read off B = omc.w with a margin (1e-6 of sum |omc_i w_i|) that covers
+     * the rounding of normalize() and of both dot products. */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return true; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &)
+    {
+        if constexpr (!SEL::take(MAT))
+            return true;
+        const float B = dot(c.omc, w);
+        const float s = (__builtin_fabsf(c.omc.x * w.x) + __builtin_fabsf(c.omc.y * w.y)) +
+                        __builtin_fabsf(c.omc.z * w.z);
+        const bool pre = c.c > 0.0f && (__builtin_fabsf(c.omc.x) + __builtin_fabsf(c.omc.y)) +
+                                               __builtin_fabsf(c.omc.z) < 1e15f;
+        return pre && B > __builtin_fmaxf(1e-6f * s, 1e-30f);
+    }
 };
 
 /* Plane half-space {p : n.p + d < 0} (src/plane.cpp:35-63).  P[OFF..] = n, d. */
@@ -493,6 +535,10 @@ struct Pln
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)
     {
         c.num = unif(-e.P[OFF + 3] - dot(o, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2])));
+    }
+    __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e)
+    {
+        c.num = -e.P[OFF + 3] - dot(o, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)
     {
@@ -547,6 +593,26 @@ struct Pln
     {
         return normalize(mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
+    /* Sound dark test on an unnormalised direction w (see Sph::dark_raw).
+     * With num <= -1e-6 the span of normalize(w) is dead or ends before EPS
+     * unless div = n.normalize(w) <= -1e-6: div in (-1e-6, 1e-6) is
+     * degenerate (dead), div >= 1e-6 gives t1 = num / div < 0 (or |t| >= 1e20,
+     * dead).  For |n|_1 <= 1.5 the computed div lies within 6.1e-7 |n|_1 <
+     * 1e-6 of (n.w) / |w| for a computed n.w >= 0, so n.w >= 0 suffices. */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return true; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &e)
+    {
+        if constexpr (!SEL::take(MAT))
+            return true;
+        const V3 np = mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
+        const bool pre = c.num <= -(EPS * EPS) &&
+                         (__builtin_fabsf(np.x) + __builtin_fabsf(np.y)) + __builtin_fabsf(np.z) <= 1.5f;
+        return pre && dot(w, np) >= 0.0f;
+    }
 };
 
 /* Binary CSG nodes: pull-protocol restatement of the reference iterators.
@@ -570,6 +636,11 @@ struct Pln
     {                                                                                               \
         A::prep(c.a, o, e);                                                                         \
         B::prep(c.b, o, e);                                                                         \
+    }                                                                                               \
+    __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e)                      \
+    {                                                                                               \
+        A::prep_l(c.a, o, e);                                                                       \
+        B::prep_l(c.b, o, e);                                                                       \
     }                                                                                               \
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)   \
     {                                                                                               \
@@ -608,6 +679,15 @@ struct Pln
         if (prim < A::HI)                                                                           \
             return A::normal(prim, t, o, d, e);                                                     \
         return B::normal(prim, t, o, d, e);                                                         \
+    }                                                                                               \
+    template <class SEL>                                                                            \
+    __device__ static constexpr bool raw_ok() { return A::template raw_ok<SEL>() && B::template raw_ok<SEL>(); } \
+    template <class SEL>                                                                            \
+    __device__ static constexpr int nsel() { return A::template nsel<SEL>() + B::template nsel<SEL>(); } \
+    template <class SEL>                                                                            \
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &e)              \
+    {                                                                                               \
+        return A::template dark_raw<SEL>(c.a, w, e) & B::template dark_raw<SEL>(c.b, w, e);         \
     }
 
 /* Each merge step decides what to emit and which child to advance, then
@@ -756,6 +836,7 @@ struct Xf
     };
     typedef typename C::St St;
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e) { C::prep(c.c, univ(m_apply(e.P + MOFF, o)), e); }
+    __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e) { C::prep_l(c.c, m_apply(e.P + MOFF, o), e); }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)
     {
         C::init(s, c.c, mkray(m_lin(e.P + MOFF, q.d)), e);
@@ -782,6 +863,13 @@ struct Xf
         V3 n = C::normal(prim, t, m_apply(e.P + MOFF, o), m_lin(e.P + MOFF, d), e);
         return normalize(m_lin(e.P + IOFF, n));
     }
+    /* no raw-direction dark test through a transform unless nothing inside is selected */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return C::template nsel<SEL>() == 0; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return C::template nsel<SEL>(); }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &, V3, const Env &) { return true; }
 };
 
 /* First qualifying span of the root, traceRay's scan (path-trace.h:66-100). */
@@ -1066,6 +1154,12 @@ struct Counters
 #define PT_CNT(c, k, v)
 #endif
 };
+/* ISA markers for static instruction counts (tools/isa_sections.py) */
+#ifdef PT_MARKERS
+#define PT_MARK(n) asm volatile("s_nop " #n)
+#else
+#define PT_MARK(n)
+#endif
 /* Per-phase wave cycle counters (profiling builds only: PT_DEVICE_DEFINES="PT_PHASE_TIMING") */
 #ifdef PT_PHASE_TIMING
 #define PT_T0(v) const u64 v = __builtin_amdgcn_s_memtime()
@@ -1078,7 +1172,8 @@ struct Counters
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
-    float4 *q;            /* PT_QCAP queued leaf-child rays (direction, factor)           */
+    V3 *q;                /* PT_QCAP queued leaf-child directions                         */
+    void *ctx;            /* the burst origin's S::Root::Ctx, prepared once per burst     */
     float4 *ring;         /* PT_RCAP kept-child slots: parked ray, then the child's term */
     u64 *gmask;           /* PT_GCAP groups of 64 children: which lanes hold a ring slot */
     unsigned char *fastq; /* PT_SCAP slots waiting for the fast pass (position mod 256) */
@@ -1109,17 +1204,18 @@ struct Frame
 enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 
 #ifndef PT_KATT
-#define PT_KATT 2 /* rejection attempts per lane per generation round */
+#define PT_KATT 4 /* rejection attempts per lane per generation round */
 #endif
-#define PT_QCAP 256 /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
+#define PT_QCAP (64 + 64 * PT_KATT) /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
 #define PT_RCAP 256 /* kept-child slots per wave awaiting their group sum          */
 #define PT_GCAP 32  /* groups per wave awaiting their sum                           */
 #define PT_SCAP 256 /* parked children per queue (byte offsets): a drain can add 2 x 64 to < 64 */
 static_assert(64 + 64 * PT_KATT <= PT_QCAP, "queue too small for PT_KATT");
-#define PT_JUMP_ENTRIES 193 /* host table: m = 0..192 attempts (PT_KATT <= 3) */
+#define PT_JUMP_ENTRIES 321 /* host table: m = 0..320 attempts */
+static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
 
 /* One rejection attempt of the scatter loop body (path-trace.h:141-158):
- * draws s0, s1, s2 are the attempt's three engine states. */
+ * s0 is the engine state before the attempt's three draws (outputs of s1, s2, s3). */
 struct Attempt
 {
     V3 wn;        /* accepted direction (unnormalised in deferred mode)      */
@@ -1133,9 +1229,10 @@ template <bool DEFERRED, bool KR0>
 __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float sc, float sNa, float abs_rc,
                                            bool child_leaf_depth)
 {
-    const u64 s1 = s0 * 214013ull + inc;
-    const u64 s2 = s1 * 214013ull + inc;
-    const V3 v = mk(__builtin_fmaf((float)(u32)(s0 >> 32), 0x1p-31f, -1.0f), __builtin_fmaf((float)(u32)(s1 >> 32), 0x1p-31f, -1.0f), __builtin_fmaf((float)(u32)(s2 >> 32), 0x1p-31f, -1.0f));
+    const u64 s1 = s0 * LCG_MULT + inc;
+    const u64 s2 = s1 * LCG_MULT + inc;
+    const u64 s3 = s2 * LCG_MULT + inc;
+    const V3 v = mk(u11(lcg_out(s1)), u11(lcg_out(s2)), u11(lcg_out(s3)));
     /* rand(): while (mag > max) with mag = sqrt(|v|^2); correctly rounded
      * sqrt(x) > 1  <=>  x > 1 + 2^-23 (exhaustively checked) */
     const bool ball = !(dot(v, v) > 0x1.000002p+0f);
@@ -1234,7 +1331,8 @@ template <class S, bool STRICT, bool DEFERRED, bool KR0>
 __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
-    float4 *const q = L.q, *const ring = L.ring;
+    V3 *const q = L.q;
+    float4 *const ring = L.ring;
     unsigned char *const fastq = L.fastq, *const slowq = L.slowq;
     const int lane = threadIdx.x & 63;
     const u64 below = (1ull << lane) - 1ull;
@@ -1252,6 +1350,15 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const u64 A64 = jump[128], g64inc = jump[129] * rng.inc;   /* 64 attempts = 192 draws  */
     const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * rng.inc; /* a full round */
     int qhead = 0, qn = 0, fails = 0, reason = -1;
+    /* x mod PT_QCAP for 0 <= x < 2 * PT_QCAP */
+    auto qwrap = [](int x) { return (int)min((u32)x, (u32)(x - PT_QCAP)); };
+    /* the burst origin's primitive contexts, shared by every pass of the burst */
+    typename S::Root::Ctx *const cxp = (typename S::Root::Ctx *)L.ctx;
+    {
+        typename S::Root::Ctx c;
+        S::Root::prep(c, hit, e);
+        *cxp = c;
+    }
     /* children are numbered in stage-A order (npos); stage A's batches of 64 are
      * the summation groups.  A DARK child (no emissive primitive reachable, and a
      * positive weight) has the burst-uniform term Z = rc * 0 and takes no ring
@@ -1267,12 +1374,20 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     /* ((aN * factor) * rc) * (+0) == rc * (+0) bitwise for any finite aN * factor > 0 */
     const V3 Z = rc * mk(0.0f, 0.0f, 0.0f);
     int fast_on = 1;
+    /* RAW: stage A decides dark children on the unnormalised direction
+     * (dark_raw, sound but conservative).  Its Z shortcut also needs a factor
+     * >= +0, i.e. a computed dot(normalize(w), n) >= 0: accepted w have a
+     * computed n.w > EPS and |w| <= 1 + |kR| (< 65), so the rounding of
+     * normalize and dot (< 7e-5 here) cannot flip the sign. */
+    constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
+    const bool raw_on = KR0 || length(kR) < 64.0f;
     u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
     PT_CNT(cnt, 0, 1);
     for (;;) {
         PT_CNT(cnt, 1, 1);
         if (reason < 0 && qn < 64) {
             PT_T0(tg);
+            PT_MARK(13);
             /* ---- generation round: lane l evaluates attempts l, 64 + l, ... */
             Attempt at[PT_KATT];
             u64 Am[PT_KATT], Fm[PT_KATT], NLm[PT_KATT];
@@ -1320,24 +1435,25 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 child.depth = depth - 1;
             }
             n_att += (u32)m;
-            int base = qhead + qn;
+            int base = qwrap(qhead + qn);
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
                 if ((take[k] >> lane) & 1ull)
-                    q[(base + __popcll(take[k] & below)) & (PT_QCAP - 1)] =
-                        make_float4(at[k].wn.x, at[k].wn.y, at[k].wn.z, at[k].factor);
-                base += __popcll(take[k]);
+                    q[qwrap(base + __popcll(take[k] & below))] = at[k].wn;
+                base = qwrap(base + __popcll(take[k]));
+                qn += __popcll(take[k]);
             }
-            qn = base - qhead;
             /* ---- advance the sample's stream past the consumed attempts */
             if (m == 64 * PT_KATT)
                 rng.st = Afull * rng.st + gfullinc;
             else
                 rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
             PT_ACC(cnt, 0, tg);
+            PT_MARK(15);
         }
         if (qn >= 64 || (reason >= 0 && qn > 0)) {
             PT_T0(ta);
+            PT_MARK(14);
             /* ---- stage A: one queued leaf child per lane.  A child whose ray no
              * emissive primitive meets at t >= eps has the term weight * (+0)
              * whatever the CSG makes of it (merges only copy primitive
@@ -1348,13 +1464,25 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             PT_CNT(cnt, 2, 1);
             int lit = 0, keep = 0;
             float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (lane < cntb) {
-                float4 en = q[(qhead + lane) & (PT_QCAP - 1)];
-                V3 dir = mk(en.x, en.y, en.z);
-                if (DEFERRED) {
-                    dir = cnormalize(dir);
-                    en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
+            if (RAW) {
+                /* every child here is a leaf: the raw test alone decides dark;
+                 * kept children park their unnormalised direction and the fast
+                 * pass normalises them, 64 useful lanes at a time */
+                if (lane < cntb) {
+                    const V3 w = q[qwrap(qhead + lane)];
+                    const typename S::Root::Ctx ctx = *cxp;
+                    keep = !(raw_on && S::Root::template dark_raw<Emissive<S>>(ctx, w, e));
+                    lit = keep;
+                    out = make_float4(w.x, w.y, w.z, 0.0f);
                 }
+            } else if (lane < cntb) {
+                V3 dir = q[qwrap(qhead + lane)];
+                if (DEFERRED)
+                    dir = cnormalize(dir);
+                /* the factor of path-trace.h:160, the same expression as at
+                 * generation in the non-deferred case */
+                float4 en;
+                en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
 #if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
                 /* experiment: generation cost only */
                 {
@@ -1365,8 +1493,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 }
 #else
                 {
-                    typename S::Root::Ctx ctx;
-                    S::Root::prep(ctx, hit, e);
+                    const typename S::Root::Ctx ctx = *cxp;
                     PrimSpans<S::Root::HI> ps;
                     S::Root::template span_sel<Emissive<S>>(ps, ctx, mkray(dir), e);
                     S::Root::template each_sel<Emissive<S>>([&](auto x) {
@@ -1403,10 +1530,11 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             n_dark += (u32)(cntb - __popcll(LM));
             npos += cntb;
             n_leaf += (u32)cntb;
-            qhead += cntb;
+            qhead = qwrap(qhead + cntb);
             qn -= cntb;
             i += cntb;
             PT_ACC(cnt, 1, ta);
+            PT_MARK(15);
         }
         const bool final = reason >= 0 && qn == 0;
         /* queued slots hold ring numbers mod 256; every pending one lies in
@@ -1426,20 +1554,36 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 /* the fast check keeps failing in this burst: park for the full merge */
                 pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
                 slow = 1;
+                if (RAW) {
+                    const float4 en = ring[pos & (PT_RCAP - 1)];
+                    const V3 dir = cnormalize(mk(en.x, en.y, en.z));
+                    ring[pos & (PT_RCAP - 1)] = make_float4(dir.x, dir.y, dir.z, 1.0f - (1.0f - dot(dir, n)) * sc);
+                }
             } else if (lane < cf) {
                 pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
-                const float4 en = ring[pos & (PT_RCAP - 1)];
+                float4 en = ring[pos & (PT_RCAP - 1)];
+                if (RAW) {
+                    /* the normalisation and factor stage A left to this pass
+                     * (the same expressions as path-trace.h:157, :160) */
+                    const V3 nd = cnormalize(mk(en.x, en.y, en.z));
+                    en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
+                }
                 const V3 dir = mk(en.x, en.y, en.z);
-                typename S::Root::Ctx ctx;
-                S::Root::prep(ctx, hit, e);
+                PT_MARK(8);
+                const typename S::Root::Ctx ctx = *cxp;
                 PrimSpans<S::Root::HI> ps;
+                PT_MARK(9);
                 S::Root::span(ps, ctx, mkray(dir), e);
-                if (S::Root::fast_ok(ps)) {
+                PT_MARK(10);
+                const int fok = S::Root::fast_ok(ps);
+                PT_MARK(11);
+                if (fok) {
                     float t = 0.0f;
                     int mat = 0;
                     V3 col = mk(0, 0, 0);
                     if (fast_first_hit<typename S::Root>(ps, t, mat))
                         col = S::emis(mat, hit + t * dir, e);
+                    PT_MARK(12);
                     const V3 term = ((aN * en.w) * rc) * col;
                     ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
                 } else {
@@ -1448,6 +1592,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     ring[pos & (PT_RCAP - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #else
                     slow = 1;
+                    if (RAW)
+                        ring[pos & (PT_RCAP - 1)] = en;
 #endif
                 }
             }
@@ -1478,8 +1624,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 const int pos = slot_pos(slowq[(s_head + lane) & (PT_SCAP - 1)]);
                 const float4 en = ring[pos & (PT_RCAP - 1)];
                 const V3 dir = mk(en.x, en.y, en.z);
-                typename S::Root::Ctx ctx;
-                S::Root::prep(ctx, hit, e);
+                const typename S::Root::Ctx ctx = *cxp;
                 float t;
                 u32 ref;
                 bool ex;
@@ -1521,6 +1666,36 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 if ((gm >> lane) & 1ull) {
                     const float4 tv = ring[(keep_sum + __popcll(gm & below)) & (PT_RCAP - 1)];
                     term = mk(tv.x, tv.y, tv.z);
+                }
+                if (!STRICT && gsum + 1 < ngrp) {
+                    /* groups finish in batches (a slow pass resolves many at
+                     * once): when the next group is finished too, its six
+                     * tree sums run interleaved with these; retval still adds
+                     * the group sums one after the other */
+                    const u64 gm2 = ((u64)(u32)uni((int)(nx >> 32)) << 32) | (u64)(u32)uni((int)nx);
+                    const int gk2 = __popcll(gm2);
+                    if (keep_sum + gk + gk2 <= resolved) {
+                        u64 nx2 = 0ull;
+                        if (gsum + 2 < ngrp)
+                            nx2 = gmask[(gsum + 2) & (PT_GCAP - 1)];
+                        const int cg2 = min(64, npos - 64 * (gsum + 1));
+                        PT_CNT(cnt, 5, 1);
+                        V3 term2 = mk(-0.0f, -0.0f, -0.0f);
+                        if (lane < cg2)
+                            term2 = Z;
+                        if ((gm2 >> lane) & 1ull) {
+                            const float4 tv = ring[(keep_sum + gk + __popcll(gm2 & below)) & (PT_RCAP - 1)];
+                            term2 = mk(tv.x, tv.y, tv.z);
+                        }
+                        const V3 g1 = mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
+                        const V3 g2 = mk(wave_tree_sum(term2.x), wave_tree_sum(term2.y), wave_tree_sum(term2.z));
+                        retval = univ(retval + g1);
+                        retval = univ(retval + g2);
+                        keep_sum += gk + gk2;
+                        gsum += 2;
+                        head_gm = ((u64)(u32)uni((int)(nx2 >> 32)) << 32) | (u64)(u32)uni((int)nx2);
+                        continue;
+                    }
                 }
                 if (STRICT) {
                     for (int j = 0; j < cg; j++)
@@ -1579,21 +1754,100 @@ enum { RS_REFRACT, RS_SCATTER };
 
 /* One sample = one traceRay tree (path-trace.h:58-165) + the jittered camera
  * ray of tracePixel (path-trace.h:190-198).  F = this wave's frame stack. */
+/* The camera query of a sample, found ahead of time by one lane of the wave
+ * (render_chunk traces a chunk's camera rays one per lane). */
+struct CamHit
+{
+    int hit;
+    float t;
+    u32 ref;
+    int ex;
+};
+
+/* tracePixel's jittered camera ray (path-trace.h:190-198): two draws */
+__device__ __forceinline__ V3 camera_dir(const PtLaunch &lp, int pix, Rng &rng)
+{
+    const int px = pix % lp.gw, py = pix / lp.gw;
+    float x = 2.0f * ((float)px + u01(rng_next(rng))) / (float)lp.W - 1.0f;
+    float y = 1.0f - 2.0f * ((float)py + u01(rng_next(rng))) / (float)lp.H;
+    return mk(x * lp.sw, y * lp.sh, -lp.dist);
+}
+
+/* A whole sample evaluated by one lane when its ray tree is the camera query
+ * plus at most one mirror child that is a leaf (sky, background and other
+ * non-scattering first hits).  Same statements as trace_sample's spine
+ * (PH_ENTER / PH_SETUP / PH_LOOP / PH_RETURN) restricted to that shape;
+ * returns false, leaving the sample to the wave, for any other shape.
+ * nq / nsh = queries / shaded hits, for the statistics. */
+template <class S>
+__device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 d, const CamHit &ch, V3 &res, int &nq,
+                                            int &nsh)
+{
+    const V3 z = mk(0, 0, 0), o = mk(0, 0, 0);
+    nq = 1, nsh = 0;
+    if (!ch.hit) {
+        res = (z + mk(0, 0, 0)) / 1.0f;
+        return true;
+    }
+    const V3 hit = o + ch.t * d;
+    const int mat = ref_mat(ch.ref);
+    V3 nn = S::Root::normal(ref_prim(ch.ref), ch.t, o, d, e);
+    if (ch.ref & FLIP)
+        nn = -nn;
+    float ior;
+    V3 n;
+    if (ch.ex) {
+        n = -nn;
+        ior = S::ior(mat, e);
+    } else {
+        n = nn;
+        ior = (float)(1.0 / (double)S::ior(mat, e));
+    }
+    const V3 retval = S::emis(mat, hit, e);
+    const float strength = 1.0f, add = 1.0f;
+    if (depth <= 0) {
+        res = (z + retval) / 1.0f;
+        return true;
+    }
+    nsh = 1;
+    const float rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
+    if (rf > EPS)
+        return false;
+    const float sc = clamp01(S::scat(mat, hit, e));
+    if (sc > EPS)
+        return false;
+    const float N = 1.0f; /* sc <= eps */
+    const V3 rc = S::refl(mat, hit, e);
+    const V3 refl = reflect(d, n);
+    const float factor = 1.0f - (1.0f - dot(refl, n)) * sc;
+    const V3 w = ((add / N) * factor) * rc;
+    const float cs = (((strength / N) * add) * factor) * length(rc);
+    if (!(depth - 1 <= 0 || cs < EPS))
+        return false;
+    nq = 2;
+    typename S::Root::Ctx ctx;
+    S::Root::prep_l(ctx, hit, e);
+    float t2 = 0.0f;
+    u32 ref2 = 0;
+    bool ex2 = false;
+    V3 col = mk(0, 0, 0);
+    if (first_hit<typename S::Root>(ctx, refl, e, t2, ref2, ex2))
+        col = S::emis(ref_mat(ref2), hit + t2 * refl, e);
+    res = (z + (retval + w * col)) / 1.0f;
+    return true;
+}
+
 template <class S, int MAXD, bool STRICT>
 __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, const WaveLds &L,
-                                           const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt)
+                                           const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt,
+                                           const CamHit &cam)
 {
     Rng rng;
     rng_seed(rng, lp.seed, (u64)pix, (u64)s);
-    const int px = pix % lp.gw, py = pix / lp.gw;
-    {
-        float x = 2.0f * ((float)px + u01(rng_next(rng))) / (float)lp.W - 1.0f;
-        float y = 1.0f - 2.0f * ((float)py + u01(rng_next(rng))) / (float)lp.H;
-        F[0].o = mk(0, 0, 0);
-        F[0].d = mk(x * lp.sw, y * lp.sh, -lp.dist);
-        F[0].strength = 1.0f;
-        F[0].depth = lp.depth;
-    }
+    F[0].o = mk(0, 0, 0);
+    F[0].d = camera_dir(lp, pix, rng);
+    F[0].strength = 1.0f;
+    F[0].depth = lp.depth;
     int sp = 0;
     int phase = PH_ENTER;
     V3 result = mk(0, 0, 0);
@@ -1602,12 +1856,18 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
         if (phase == PH_ENTER) {
             cnt.queries++;
             const V3 o = univ(f.o), d = univ(f.d);
-            typename S::Root::Ctx ctx;
-            S::Root::prep(ctx, o, e);
             float t = 0.0f;
             u32 ref = 0;
             bool ex = false;
-            if (!first_hit<typename S::Root>(ctx, d, e, t, ref, ex)) {
+            bool found;
+            if (sp == 0) {
+                found = cam.hit != 0, t = cam.t, ref = cam.ref, ex = cam.ex != 0;
+            } else {
+                typename S::Root::Ctx ctx;
+                S::Root::prep(ctx, o, e);
+                found = first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+            }
+            if (!found) {
                 result = mk(0, 0, 0);
                 phase = PH_RETURN;
                 continue;
@@ -1742,7 +2002,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                                              const PtLaunch &lp)
 {
     __shared__ Frame stk[PT_WPW][MAXD + 1];
-    __shared__ float4 qbuf[PT_WPW][PT_QCAP];
+    __shared__ V3 qbuf[PT_WPW][PT_QCAP];
+    __shared__ typename S::Root::Ctx xbuf[PT_WPW];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
     __shared__ u64 gbuf[PT_WPW][PT_GCAP];
     __shared__ unsigned char fbuf[PT_WPW][PT_SCAP];
@@ -1759,7 +2020,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
 #endif
-    const WaveLds L = {qbuf[wave], rbuf[wave], gbuf[wave], fbuf[wave], sbuf[wave]};
+    const WaveLds L = {qbuf[wave], &xbuf[wave], rbuf[wave], gbuf[wave], fbuf[wave], sbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
@@ -1771,7 +2032,33 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         if (chunk >= n_chunks)
             break;
         const long long item0 = chunk * CH;
-        V3 mine = mk(0, 0, 0);
+        /* the chunk's camera queries, one per lane */
+        CamHit ch = {0, 0.0f, 0u, 0};
+        int ldone = 0, lq = 0, lsh = 0;
+        V3 lres = mk(0, 0, 0);
+        if (lane < CH && item0 + lane < lp.n_items) {
+            const long long item = item0 + lane;
+            const long long slot = item / lp.nsamp;
+            const int s = lp.s0 + (int)(item - slot * lp.nsamp);
+            const int pix = pixels ? pixels[slot] : (int)slot;
+            Rng r;
+            rng_seed(r, lp.seed, (u64)pix, (u64)s);
+            const V3 d = camera_dir(lp, pix, r);
+            typename S::Root::Ctx ctx;
+            S::Root::prep(ctx, mk(0, 0, 0), e);
+            bool ex = false;
+            ch.hit = first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
+            ch.ex = ex ? 1 : 0;
+            ldone = lane_sample<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
+        }
+        {
+            /* statistics of the samples finished by their lane */
+            const u64 D = __ballot(ldone), Q2 = __ballot(ldone && lq == 2), SH = __ballot(ldone && lsh);
+            cnt.queries += (u64)(__popcll(D) + __popcll(Q2));
+            cnt.shaded += (u64)__popcll(SH);
+        }
+        const u64 DONE = __ballot(ldone);
+        V3 mine = lres; /* valid where ldone */
         for (int j = 0; j < CH; j++) {
             const long long item = item0 + j;
             if (item >= lp.n_items)
@@ -1779,9 +2066,12 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             const long long slot = item / lp.nsamp;
             const int s = lp.s0 + (int)(item - slot * lp.nsamp);
             const int pix = pixels ? pixels[slot] : (int)slot;
+            if ((DONE >> j) & 1ull)
+                continue;
             PT_T0(tt);
-            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], L, jump, A3l, G3l,
-                                                 cnt);
+            const CamHit cam = {__builtin_amdgcn_readlane(ch.hit, j), rdlane(ch.t, j),
+                                (u32)__builtin_amdgcn_readlane((int)ch.ref, j), __builtin_amdgcn_readlane(ch.ex, j)};
+            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], L, jump, A3l, G3l, cnt, cam);
             PT_ACC(cnt, 6, tt);
             if (lane == j)
                 mine = c;
@@ -1814,7 +2104,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
 } // namespace ptd
 
 #ifndef PT_MIN_WAVES
-#define PT_MIN_WAVES 1
+#define PT_MIN_WAVES 4 /* 4 workgroups of 4 waves per CU: caps VGPRs at 128 (4 waves/SIMD) */
 #endif
 
 #define PT_RENDER_ARGS                                                                                     \

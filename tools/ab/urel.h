@@ -1,4 +1,3 @@
-#define PT_KATT 3
 /*
  * pt_device.h -- CDNA4 (gfx950) device library of the MI355X path tracer.
  *
@@ -314,14 +313,26 @@ __device__ __forceinline__ float dpp_partner(float v)
 {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+/* v + src broadcast from the last lane of the row(s) below, on rows ROWS only;
+ * the other rows add -0.0f, which leaves every value (and the sign of 0) */
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_bcast_add(float v)
+{
+    return v + __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(-0.0f), __float_as_int(v), CTRL, ROWS, 0xF,
+                                                          false));
+}
 __device__ __forceinline__ float wave_tree_sum(float v)
 {
     v = v + dpp_partner<0xB1>(v);  /* quad_perm [1,0,3,2]: lane ^ 1 */
     v = v + dpp_partner<0x4E>(v);  /* quad_perm [2,3,0,1]: lane ^ 2 */
     v = v + dpp_partner<0x141>(v); /* row_half_mirror: partner in the other quad of the 8 */
     v = v + dpp_partner<0x140>(v); /* row_mirror: partner in the other 8 of the row */
-    float r0 = rdlane(v, 0), r1 = rdlane(v, 16), r2 = rdlane(v, 32), r3 = rdlane(v, 48);
-    return (r0 + r1) + (r2 + r3);
+    /* rows now hold r0..r3 in every lane; row_bcast:15 gives rows 1 and 3
+     * r1 + r0 and r3 + r2, row_bcast:31 gives row 3 (r3 + r2) + (r1 + r0):
+     * by commutativity the bits of (r0 + r1) + (r2 + r3) */
+    v = dpp_bcast_add<0x142, 0xA>(v);
+    v = dpp_bcast_add<0x143, 0x8>(v);
+    return rdlane(v, 63);
 }
 
 /* ----------------------------------------------------------- CSG spans --- */
@@ -393,6 +404,22 @@ __device__ __forceinline__ int sep(const PS &ps, int x, int y)
 {
     return (!ps.live[x]) | (!ps.live[y]) | (ps.t1[x] < ps.t0[y]) | (ps.t1[y] < ps.t0[x]) |
            ((ps.t1[x] < EPS) & (ps.t1[y] < EPS));
+}
+/* At a Union node (src/union.cpp:84-134) overlapping spans merge into one
+ * whose start is the earlier start (the B side's on a tie, :125-132); when
+ * both starts are >= EPS and differ, that merged span begins at the smaller
+ * start >= EPS, so traceRay's scan stops at it exactly as at the earlier
+ * span alone -- what fast_first_hit picks.  (A third span separated from both
+ * lies wholly before or after their merge.)  Such pairs pass too: unions of
+ * overlapping half-spaces (C2/C5's sky box, ground planes) stay on the fast
+ * pass.  Difference and Intersection nodes keep the strict rule. */
+template <bool UNION, class PS>
+__device__ __forceinline__ int pair_ok(const PS &ps, int x, int y)
+{
+    int ok = sep(ps, x, y);
+    if (UNION)
+        ok |= (ps.t0[x] >= EPS) & (ps.t0[y] >= EPS) & (ps.t0[x] != ps.t0[y]);
+    return ok;
 }
 
 /* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r.  Branch-free:
@@ -476,6 +503,28 @@ struct Sph
     {
         return normalize((o + t * d) - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
+    /* Sound test on an UNNORMALISED direction w that the span of normalize(w)
+     * is dead or ends before EPS (stage A of the scatter loop).  Origin
+     * outside (c > 0) and receding (b > 0): disc = fl(fl(b*b) - a*c) <= fl(b*b),
+     * so sqrt(disc) <= b and t1 = (-b + sqrt(disc)) / a <= 0.  b's sign is
+     * read off B = omc.w with a margin (1e-6 of sum |omc_i w_i|) that covers
+     * the rounding of normalize() and of both dot products. */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return true; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &)
+    {
+        if constexpr (!SEL::take(MAT))
+            return true;
+        const float B = dot(c.omc, w);
+        const float s = (__builtin_fabsf(c.omc.x * w.x) + __builtin_fabsf(c.omc.y * w.y)) +
+                        __builtin_fabsf(c.omc.z * w.z);
+        const bool pre = c.c > 0.0f && (__builtin_fabsf(c.omc.x) + __builtin_fabsf(c.omc.y)) +
+                                               __builtin_fabsf(c.omc.z) < 1e15f;
+        return pre && B > __builtin_fmaxf(1e-6f * s, 1e-30f);
+    }
 };
 
 /* Plane half-space {p : n.p + d < 0} (src/plane.cpp:35-63).  P[OFF..] = n, d. */
@@ -553,6 +602,26 @@ struct Pln
     {
         return normalize(mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
+    /* Sound dark test on an unnormalised direction w (see Sph::dark_raw).
+     * With num <= -1e-6 the span of normalize(w) is dead or ends before EPS
+     * unless div = n.normalize(w) <= -1e-6: div in (-1e-6, 1e-6) is
+     * degenerate (dead), div >= 1e-6 gives t1 = num / div < 0 (or |t| >= 1e20,
+     * dead).  For |n|_1 <= 1.5 the computed div lies within 6.1e-7 |n|_1 <
+     * 1e-6 of (n.w) / |w| for a computed n.w >= 0, so n.w >= 0 suffices. */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return true; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &e)
+    {
+        if constexpr (!SEL::take(MAT))
+            return true;
+        const V3 np = mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
+        const bool pre = c.num <= -(EPS * EPS) &&
+                         (__builtin_fabsf(np.x) + __builtin_fabsf(np.y)) + __builtin_fabsf(np.z) <= 1.5f;
+        return pre && dot(w, np) >= 0.0f;
+    }
 };
 
 /* Binary CSG nodes: pull-protocol restatement of the reference iterators.
@@ -611,7 +680,7 @@ struct Pln
     __device__ static __forceinline__ int fast_ok(const PS &ps)                                     \
     {                                                                                               \
         int ok = A::fast_ok(ps) & B::fast_ok(ps);                                                   \
-        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= sep(ps, decltype(x)::value, decltype(y)::value); }); }); \
+        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= pair_ok<IS_UNION>(ps, decltype(x)::value, decltype(y)::value); }); }); \
         return ok;                                                                                  \
     }                                                                                               \
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)       \
@@ -619,6 +688,15 @@ struct Pln
         if (prim < A::HI)                                                                           \
             return A::normal(prim, t, o, d, e);                                                     \
         return B::normal(prim, t, o, d, e);                                                         \
+    }                                                                                               \
+    template <class SEL>                                                                            \
+    __device__ static constexpr bool raw_ok() { return A::template raw_ok<SEL>() && B::template raw_ok<SEL>(); } \
+    template <class SEL>                                                                            \
+    __device__ static constexpr int nsel() { return A::template nsel<SEL>() + B::template nsel<SEL>(); } \
+    template <class SEL>                                                                            \
+    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &e)              \
+    {                                                                                               \
+        return A::template dark_raw<SEL>(c.a, w, e) & B::template dark_raw<SEL>(c.b, w, e);         \
     }
 
 /* Each merge step decides what to emit and which child to advance, then
@@ -629,6 +707,7 @@ struct Pln
 template <class A, class B>
 struct Uni
 {
+    static constexpr bool IS_UNION = true;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f)
@@ -673,6 +752,7 @@ struct Uni
 template <class A, class B>
 struct Isect
 {
+    static constexpr bool IS_UNION = false;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&) {}
@@ -713,6 +793,7 @@ struct Isect
 template <class A, class B>
 struct Diff
 {
+    static constexpr bool IS_UNION = false;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { A::each_pos(f); }
@@ -794,6 +875,13 @@ struct Xf
         V3 n = C::normal(prim, t, m_apply(e.P + MOFF, o), m_lin(e.P + MOFF, d), e);
         return normalize(m_lin(e.P + IOFF, n));
     }
+    /* no raw-direction dark test through a transform unless nothing inside is selected */
+    template <class SEL>
+    __device__ static constexpr bool raw_ok() { return C::template nsel<SEL>() == 0; }
+    template <class SEL>
+    __device__ static constexpr int nsel() { return C::template nsel<SEL>(); }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_raw(const Ctx &, V3, const Env &) { return true; }
 };
 
 /* First qualifying span of the root, traceRay's scan (path-trace.h:66-100). */
@@ -1128,7 +1216,7 @@ struct Frame
 enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 
 #ifndef PT_KATT
-#define PT_KATT 2 /* rejection attempts per lane per generation round */
+#define PT_KATT 4 /* rejection attempts per lane per generation round */
 #endif
 #define PT_QCAP (64 + 64 * PT_KATT) /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
 #define PT_RCAP 256 /* kept-child slots per wave awaiting their group sum          */
@@ -1298,12 +1386,20 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     /* ((aN * factor) * rc) * (+0) == rc * (+0) bitwise for any finite aN * factor > 0 */
     const V3 Z = rc * mk(0.0f, 0.0f, 0.0f);
     int fast_on = 1;
+    /* RAW: stage A decides dark children on the unnormalised direction
+     * (dark_raw, sound but conservative).  Its Z shortcut also needs a factor
+     * >= +0, i.e. a computed dot(normalize(w), n) >= 0: accepted w have a
+     * computed n.w > EPS and |w| <= 1 + |kR| (< 65), so the rounding of
+     * normalize and dot (< 7e-5 here) cannot flip the sign. */
+    constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
+    const bool raw_on = KR0 || length(kR) < 64.0f;
     u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
     PT_CNT(cnt, 0, 1);
     for (;;) {
         PT_CNT(cnt, 1, 1);
         if (reason < 0 && qn < 64) {
             PT_T0(tg);
+            PT_MARK(13);
             /* ---- generation round: lane l evaluates attempts l, 64 + l, ... */
             Attempt at[PT_KATT];
             u64 Am[PT_KATT], Fm[PT_KATT], NLm[PT_KATT];
@@ -1365,9 +1461,11 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             else
                 rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
             PT_ACC(cnt, 0, tg);
+            PT_MARK(15);
         }
         if (qn >= 64 || (reason >= 0 && qn > 0)) {
             PT_T0(ta);
+            PT_MARK(14);
             /* ---- stage A: one queued leaf child per lane.  A child whose ray no
              * emissive primitive meets at t >= eps has the term weight * (+0)
              * whatever the CSG makes of it (merges only copy primitive
@@ -1378,7 +1476,18 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             PT_CNT(cnt, 2, 1);
             int lit = 0, keep = 0;
             float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (lane < cntb) {
+            if (RAW) {
+                /* every child here is a leaf: the raw test alone decides dark;
+                 * kept children park their unnormalised direction and the fast
+                 * pass normalises them, 64 useful lanes at a time */
+                if (lane < cntb) {
+                    const V3 w = q[qwrap(qhead + lane)];
+                    const typename S::Root::Ctx ctx = *cxp;
+                    keep = !(raw_on && S::Root::template dark_raw<Emissive<S>>(ctx, w, e));
+                    lit = keep;
+                    out = make_float4(w.x, w.y, w.z, 0.0f);
+                }
+            } else if (lane < cntb) {
                 V3 dir = q[qwrap(qhead + lane)];
                 if (DEFERRED)
                     dir = cnormalize(dir);
@@ -1437,6 +1546,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             qn -= cntb;
             i += cntb;
             PT_ACC(cnt, 1, ta);
+            PT_MARK(15);
         }
         const bool final = reason >= 0 && qn == 0;
         /* queued slots hold ring numbers mod 256; every pending one lies in
@@ -1456,9 +1566,20 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 /* the fast check keeps failing in this burst: park for the full merge */
                 pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
                 slow = 1;
+                if (RAW) {
+                    const float4 en = ring[pos & (PT_RCAP - 1)];
+                    const V3 dir = cnormalize(mk(en.x, en.y, en.z));
+                    ring[pos & (PT_RCAP - 1)] = make_float4(dir.x, dir.y, dir.z, 1.0f - (1.0f - dot(dir, n)) * sc);
+                }
             } else if (lane < cf) {
                 pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
-                const float4 en = ring[pos & (PT_RCAP - 1)];
+                float4 en = ring[pos & (PT_RCAP - 1)];
+                if (RAW) {
+                    /* the normalisation and factor stage A left to this pass
+                     * (the same expressions as path-trace.h:157, :160) */
+                    const V3 nd = cnormalize(mk(en.x, en.y, en.z));
+                    en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
+                }
                 const V3 dir = mk(en.x, en.y, en.z);
                 PT_MARK(8);
                 const typename S::Root::Ctx ctx = *cxp;
@@ -1483,6 +1604,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     ring[pos & (PT_RCAP - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #else
                     slow = 1;
+                    if (RAW)
+                        ring[pos & (PT_RCAP - 1)] = en;
 #endif
                 }
             }
@@ -1555,6 +1678,36 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 if ((gm >> lane) & 1ull) {
                     const float4 tv = ring[(keep_sum + __popcll(gm & below)) & (PT_RCAP - 1)];
                     term = mk(tv.x, tv.y, tv.z);
+                }
+                if (!STRICT && gsum + 1 < ngrp) {
+                    /* groups finish in batches (a slow pass resolves many at
+                     * once): when the next group is finished too, its six
+                     * tree sums run interleaved with these; retval still adds
+                     * the group sums one after the other */
+                    const u64 gm2 = ((u64)(u32)uni((int)(nx >> 32)) << 32) | (u64)(u32)uni((int)nx);
+                    const int gk2 = __popcll(gm2);
+                    if (keep_sum + gk + gk2 <= resolved) {
+                        u64 nx2 = 0ull;
+                        if (gsum + 2 < ngrp)
+                            nx2 = gmask[(gsum + 2) & (PT_GCAP - 1)];
+                        const int cg2 = min(64, npos - 64 * (gsum + 1));
+                        PT_CNT(cnt, 5, 1);
+                        V3 term2 = mk(-0.0f, -0.0f, -0.0f);
+                        if (lane < cg2)
+                            term2 = Z;
+                        if ((gm2 >> lane) & 1ull) {
+                            const float4 tv = ring[(keep_sum + gk + __popcll(gm2 & below)) & (PT_RCAP - 1)];
+                            term2 = mk(tv.x, tv.y, tv.z);
+                        }
+                        const V3 g1 = mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
+                        const V3 g2 = mk(wave_tree_sum(term2.x), wave_tree_sum(term2.y), wave_tree_sum(term2.z));
+                        retval = univ(retval + g1);
+                        retval = univ(retval + g2);
+                        keep_sum += gk + gk2;
+                        gsum += 2;
+                        head_gm = ((u64)(u32)uni((int)(nx2 >> 32)) << 32) | (u64)(u32)uni((int)nx2);
+                        continue;
+                    }
                 }
                 if (STRICT) {
                     for (int j = 0; j < cg; j++)
