@@ -173,6 +173,11 @@ __device__ __forceinline__ float cdiv(float n, const Rcp &R, bool dok)
  * branch, so a rarely needed slow path costs one compare-and-branch instead
  * of exec-mask bookkeeping or an if-converted second evaluation. */
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
+/* Marks a rarely taken wave-uniform fallback block: the empty volatile asm
+ * keeps LLVM from if-converting it, which would evaluate the slow exact
+ * sequence (v_div_scale / v_div_fmas / v_div_fixup, scaled sqrt) on every
+ * pass and select. */
+#define PT_COLD() asm volatile("")
 
 
 __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
@@ -181,6 +186,7 @@ __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
     float m = sqrt_core(x);
     const bool sbad = !sqrt_core_ok(x);
     if (wave_any(sbad)) {
+        PT_COLD();
         if (sbad)
             m = __builtin_sqrtf(x);
     }
@@ -190,6 +196,7 @@ __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
     V3 q = mk(div_core(v.x, R), div_core(v.y, R), div_core(v.z, R));
     const bool dbad = !(den_ok(m) && num_ok(v.x) && num_ok(v.y) && num_ok(v.z));
     if (wave_any(dbad)) {
+        PT_COLD();
         if (dbad)
             q = mk(v.x / m, v.y / m, v.z / m);
     }
@@ -470,6 +477,7 @@ struct Sph
         float t0 = div_core(n0, q.ra), t1 = div_core(n1, q.ra);
         const bool bad = live && !(q.aok && num_ok(n0) && num_ok(n1));
         if (wave_any(bad)) {
+        PT_COLD();
             if (bad)
                 t0 = n0 / q.a, t1 = n1 / q.a;
         }
@@ -566,6 +574,7 @@ struct Pln
         float t = div_core(c.num, mkrcp(div));
         const bool bad = !small && !(den_ok(div) && num_ok(c.num));
         if (wave_any(bad)) {
+        PT_COLD();
             if (bad)
                 t = c.num / div;
         }
@@ -1191,6 +1200,14 @@ struct Counters
 #define PT_ACC(c, k, v)
 #endif
 
+/* Statistics live in the wave's LDS Counters; lane 0 adds without a return
+ * value (ds_add_u64), so no register carries them through the hot loops. */
+__device__ __forceinline__ void cadd(u64 &c, u32 v)
+{
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_add(&c, (u64)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
@@ -1263,8 +1280,11 @@ __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float s
     const V3 w = KR0 ? v : v + kR;
     const bool hemi = !(dot(n, w) <= EPS); /* while (dot(normal, dir) <= eps) */
     Attempt a;
-    a.A = __ballot(ball && hemi);
-    a.F = __ballot(ball && !hemi);
+    /* one ballot per compare (a ballot of a combined predicate is lowered
+     * through a v_cndmask / v_cmp round trip) */
+    const u64 BB = __ballot(ball), HB = __ballot(hemi);
+    a.A = BB & HB;
+    a.F = BB & ~HB;
     a.wn = w;
     a.factor = 0.0f;
     a.NL = 0ull;
@@ -1403,7 +1423,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
      * normalize and dot (< 7e-5 here) cannot flip the sign. */
     constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
     const bool raw_on = KR0 || length(kR) < 64.0f;
-    u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
     PT_CNT(cnt, 0, 1);
     for (;;) {
         PT_CNT(cnt, 1, 1);
@@ -1425,7 +1444,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     NLm[k] = at[k].NL;
                 }
             }
-            n_rounds++;
+            cadd(cnt.rounds, 1u);
             /* ---- replay the sequential consumption rule on the masks */
             int rem = N - (i + qn);
             u64 take[PT_KATT];
@@ -1456,7 +1475,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 child.strength = (sNa * nf) * abs_rc;
                 child.depth = depth - 1;
             }
-            n_att += (u32)m;
+            cadd(cnt.attempts, (u32)m);
             int base = qwrap(qhead + qn);
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
@@ -1549,9 +1568,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             ngrp++;
             nkeep += __popcll(KM);
             f_n += __popcll(LM);
-            n_dark += (u32)(cntb - __popcll(LM));
+            cadd(cnt.dark, (u32)(cntb - __popcll(LM)));
             npos += cntb;
-            n_leaf += (u32)cntb;
+            cadd(cnt.leaf, (u32)cntb);
             qhead = qwrap(qhead + cntb);
             qn -= cntb;
             i += cntb;
@@ -1625,7 +1644,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             if (s_n == 0 && SM)
                 s_first = __builtin_amdgcn_readlane(pos, __builtin_ctzll(SM));
             s_n += __popcll(SM);
-            n_slow += (u32)__popcll(SM);
+            cadd(cnt.slow, (u32)__popcll(SM));
             /* overlap-heavy scenes (e.g. a box of sky half-spaces) stop trying */
             if (fast_on && 4 * __popcll(SM) > 3 * cf)
                 fast_on = 0;
@@ -1737,11 +1756,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     }
     f.retval = retval;
     f.i = i;
-    cnt.rounds += n_rounds;
-    cnt.attempts += n_att;
-    cnt.leaf += n_leaf;
-    cnt.slow += n_slow;
-    cnt.dark += n_dark;
     return reason;
 }
 

@@ -405,6 +405,32 @@ __device__ __forceinline__ int sep(const PS &ps, int x, int y)
     return (!ps.live[x]) | (!ps.live[y]) | (ps.t1[x] < ps.t0[y]) | (ps.t1[y] < ps.t0[x]) |
            ((ps.t1[x] < EPS) & (ps.t1[y] < EPS));
 }
+/* At a Union node (src/union.cpp:84-134) overlapping spans merge into one
+ * whose start is the earlier start (the B side's on a tie, :125-132); when
+ * both starts are >= EPS and differ, that merged span begins at the smaller
+ * start >= EPS, so traceRay's scan stops at it exactly as at the earlier
+ * span alone -- what fast_first_hit picks.  (A third span separated from both
+ * lies wholly before or after their merge.)  Such pairs pass too: unions of
+ * overlapping half-spaces (C2/C5's sky box, ground planes) stay on the fast
+ * pass.
+ * At a Difference node (src/difference.cpp:84-135) a B span y that starts
+ * strictly after an A span x starting at >= EPS cuts x to [x0, y0] (and
+ * maybe [y1, x1] after it): the output still begins at x's own start, and
+ * the part before it is a subset of x, so every check made against x above
+ * stays valid.  (y starting at or before x0 -- B covering x, or the :124-130
+ * quirk's inverted span -- keeps the strict rule.)  Intersection nodes keep
+ * the strict rule: separation there means an empty intersection. */
+enum { NODE_ISECT = 0, NODE_UNION = 1, NODE_DIFF = 2 };
+template <int KIND, class PS>
+__device__ __forceinline__ int pair_ok(const PS &ps, int x, int y)
+{
+    int ok = sep(ps, x, y);
+    if (KIND == NODE_UNION)
+        ok |= (ps.t0[x] >= EPS) & (ps.t0[y] >= EPS) & (ps.t0[x] != ps.t0[y]);
+    if (KIND == NODE_DIFF)
+        ok |= (ps.t0[x] >= EPS) & (ps.t0[y] > ps.t0[x]);
+    return ok;
+}
 
 /* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r.  Branch-free:
  * t0/t1 are computed on every lane (dead lanes' values are never read), with
@@ -664,7 +690,7 @@ struct Pln
     __device__ static __forceinline__ int fast_ok(const PS &ps)                                     \
     {                                                                                               \
         int ok = A::fast_ok(ps) & B::fast_ok(ps);                                                   \
-        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= sep(ps, decltype(x)::value, decltype(y)::value); }); }); \
+        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= pair_ok<KIND>(ps, decltype(x)::value, decltype(y)::value); }); }); \
         return ok;                                                                                  \
     }                                                                                               \
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)       \
@@ -691,6 +717,7 @@ struct Pln
 template <class A, class B>
 struct Uni
 {
+    static constexpr int KIND = NODE_UNION;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f)
@@ -735,6 +762,7 @@ struct Uni
 template <class A, class B>
 struct Isect
 {
+    static constexpr int KIND = NODE_ISECT;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&) {}
@@ -775,6 +803,7 @@ struct Isect
 template <class A, class B>
 struct Diff
 {
+    static constexpr int KIND = NODE_DIFF;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { A::each_pos(f); }

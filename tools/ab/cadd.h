@@ -1191,6 +1191,14 @@ struct Counters
 #define PT_ACC(c, k, v)
 #endif
 
+/* Statistics live in the wave's LDS Counters; lane 0 adds without a return
+ * value (ds_add_u64), so no register carries them through the hot loops. */
+__device__ __forceinline__ void cadd(u64 &c, u32 v)
+{
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_add(&c, (u64)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
@@ -1403,7 +1411,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
      * normalize and dot (< 7e-5 here) cannot flip the sign. */
     constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
     const bool raw_on = KR0 || length(kR) < 64.0f;
-    u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
     PT_CNT(cnt, 0, 1);
     for (;;) {
         PT_CNT(cnt, 1, 1);
@@ -1425,7 +1432,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     NLm[k] = at[k].NL;
                 }
             }
-            n_rounds++;
+            cadd(cnt.rounds, 1u);
             /* ---- replay the sequential consumption rule on the masks */
             int rem = N - (i + qn);
             u64 take[PT_KATT];
@@ -1456,7 +1463,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 child.strength = (sNa * nf) * abs_rc;
                 child.depth = depth - 1;
             }
-            n_att += (u32)m;
+            cadd(cnt.attempts, (u32)m);
             int base = qwrap(qhead + qn);
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
@@ -1549,9 +1556,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             ngrp++;
             nkeep += __popcll(KM);
             f_n += __popcll(LM);
-            n_dark += (u32)(cntb - __popcll(LM));
+            cadd(cnt.dark, (u32)(cntb - __popcll(LM)));
             npos += cntb;
-            n_leaf += (u32)cntb;
+            cadd(cnt.leaf, (u32)cntb);
             qhead = qwrap(qhead + cntb);
             qn -= cntb;
             i += cntb;
@@ -1625,7 +1632,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             if (s_n == 0 && SM)
                 s_first = __builtin_amdgcn_readlane(pos, __builtin_ctzll(SM));
             s_n += __popcll(SM);
-            n_slow += (u32)__popcll(SM);
+            cadd(cnt.slow, (u32)__popcll(SM));
             /* overlap-heavy scenes (e.g. a box of sky half-spaces) stop trying */
             if (fast_on && 4 * __popcll(SM) > 3 * cf)
                 fast_on = 0;
@@ -1737,11 +1744,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     }
     f.retval = retval;
     f.i = i;
-    cnt.rounds += n_rounds;
-    cnt.attempts += n_att;
-    cnt.leaf += n_leaf;
-    cnt.slow += n_slow;
-    cnt.dark += n_dark;
     return reason;
 }
 

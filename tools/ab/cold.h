@@ -173,6 +173,11 @@ __device__ __forceinline__ float cdiv(float n, const Rcp &R, bool dok)
  * branch, so a rarely needed slow path costs one compare-and-branch instead
  * of exec-mask bookkeeping or an if-converted second evaluation. */
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
+/* Marks a rarely taken wave-uniform fallback block: the empty volatile asm
+ * keeps LLVM from if-converting it, which would evaluate the slow exact
+ * sequence (v_div_scale / v_div_fmas / v_div_fixup, scaled sqrt) on every
+ * pass and select. */
+#define PT_COLD() asm volatile("")
 
 
 __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
@@ -181,6 +186,7 @@ __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
     float m = sqrt_core(x);
     const bool sbad = !sqrt_core_ok(x);
     if (wave_any(sbad)) {
+        PT_COLD();
         if (sbad)
             m = __builtin_sqrtf(x);
     }
@@ -190,6 +196,7 @@ __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
     V3 q = mk(div_core(v.x, R), div_core(v.y, R), div_core(v.z, R));
     const bool dbad = !(den_ok(m) && num_ok(v.x) && num_ok(v.y) && num_ok(v.z));
     if (wave_any(dbad)) {
+        PT_COLD();
         if (dbad)
             q = mk(v.x / m, v.y / m, v.z / m);
     }
@@ -412,13 +419,23 @@ __device__ __forceinline__ int sep(const PS &ps, int x, int y)
  * span alone -- what fast_first_hit picks.  (A third span separated from both
  * lies wholly before or after their merge.)  Such pairs pass too: unions of
  * overlapping half-spaces (C2/C5's sky box, ground planes) stay on the fast
- * pass.  Difference and Intersection nodes keep the strict rule. */
-template <bool UNION, class PS>
+ * pass.
+ * At a Difference node (src/difference.cpp:84-135) a B span y that starts
+ * strictly after an A span x starting at >= EPS cuts x to [x0, y0] (and
+ * maybe [y1, x1] after it): the output still begins at x's own start, and
+ * the part before it is a subset of x, so every check made against x above
+ * stays valid.  (y starting at or before x0 -- B covering x, or the :124-130
+ * quirk's inverted span -- keeps the strict rule.)  Intersection nodes keep
+ * the strict rule: separation there means an empty intersection. */
+enum { NODE_ISECT = 0, NODE_UNION = 1, NODE_DIFF = 2 };
+template <int KIND, class PS>
 __device__ __forceinline__ int pair_ok(const PS &ps, int x, int y)
 {
     int ok = sep(ps, x, y);
-    if (UNION)
+    if (KIND == NODE_UNION)
         ok |= (ps.t0[x] >= EPS) & (ps.t0[y] >= EPS) & (ps.t0[x] != ps.t0[y]);
+    if (KIND == NODE_DIFF)
+        ok |= (ps.t0[x] >= EPS) & (ps.t0[y] > ps.t0[x]);
     return ok;
 }
 
@@ -460,6 +477,7 @@ struct Sph
         float t0 = div_core(n0, q.ra), t1 = div_core(n1, q.ra);
         const bool bad = live && !(q.aok && num_ok(n0) && num_ok(n1));
         if (wave_any(bad)) {
+        PT_COLD();
             if (bad)
                 t0 = n0 / q.a, t1 = n1 / q.a;
         }
@@ -556,6 +574,7 @@ struct Pln
         float t = div_core(c.num, mkrcp(div));
         const bool bad = !small && !(den_ok(div) && num_ok(c.num));
         if (wave_any(bad)) {
+        PT_COLD();
             if (bad)
                 t = c.num / div;
         }
@@ -680,7 +699,7 @@ struct Pln
     __device__ static __forceinline__ int fast_ok(const PS &ps)                                     \
     {                                                                                               \
         int ok = A::fast_ok(ps) & B::fast_ok(ps);                                                   \
-        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= pair_ok<IS_UNION>(ps, decltype(x)::value, decltype(y)::value); }); }); \
+        A::each_pos([&](auto x, auto) { B::each_pos([&](auto y, auto) { ok &= pair_ok<KIND>(ps, decltype(x)::value, decltype(y)::value); }); }); \
         return ok;                                                                                  \
     }                                                                                               \
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)       \
@@ -707,7 +726,7 @@ struct Pln
 template <class A, class B>
 struct Uni
 {
-    static constexpr bool IS_UNION = true;
+    static constexpr int KIND = NODE_UNION;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f)
@@ -752,7 +771,7 @@ struct Uni
 template <class A, class B>
 struct Isect
 {
-    static constexpr bool IS_UNION = false;
+    static constexpr int KIND = NODE_ISECT;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&) {}
@@ -793,7 +812,7 @@ struct Isect
 template <class A, class B>
 struct Diff
 {
-    static constexpr bool IS_UNION = false;
+    static constexpr int KIND = NODE_DIFF;
     PTD_BINARY_COMMON
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { A::each_pos(f); }
@@ -1181,6 +1200,14 @@ struct Counters
 #define PT_ACC(c, k, v)
 #endif
 
+/* Statistics live in the wave's LDS Counters; lane 0 adds without a return
+ * value (ds_add_u64), so no register carries them through the hot loops. */
+__device__ __forceinline__ void cadd(u64 &c, u32 v)
+{
+    if ((threadIdx.x & 63) == 0)
+        __hip_atomic_fetch_add(&c, (u64)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
@@ -1253,8 +1280,11 @@ __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float s
     const V3 w = KR0 ? v : v + kR;
     const bool hemi = !(dot(n, w) <= EPS); /* while (dot(normal, dir) <= eps) */
     Attempt a;
-    a.A = __ballot(ball && hemi);
-    a.F = __ballot(ball && !hemi);
+    /* one ballot per compare (a ballot of a combined predicate is lowered
+     * through a v_cndmask / v_cmp round trip) */
+    const u64 BB = __ballot(ball), HB = __ballot(hemi);
+    a.A = BB & HB;
+    a.F = BB & ~HB;
     a.wn = w;
     a.factor = 0.0f;
     a.NL = 0ull;
@@ -1393,7 +1423,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
      * normalize and dot (< 7e-5 here) cannot flip the sign. */
     constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
     const bool raw_on = KR0 || length(kR) < 64.0f;
-    u32 n_rounds = 0, n_att = 0, n_leaf = 0, n_slow = 0, n_dark = 0;
     PT_CNT(cnt, 0, 1);
     for (;;) {
         PT_CNT(cnt, 1, 1);
@@ -1415,7 +1444,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     NLm[k] = at[k].NL;
                 }
             }
-            n_rounds++;
+            cadd(cnt.rounds, 1u);
             /* ---- replay the sequential consumption rule on the masks */
             int rem = N - (i + qn);
             u64 take[PT_KATT];
@@ -1446,7 +1475,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 child.strength = (sNa * nf) * abs_rc;
                 child.depth = depth - 1;
             }
-            n_att += (u32)m;
+            cadd(cnt.attempts, (u32)m);
             int base = qwrap(qhead + qn);
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
@@ -1539,9 +1568,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             ngrp++;
             nkeep += __popcll(KM);
             f_n += __popcll(LM);
-            n_dark += (u32)(cntb - __popcll(LM));
+            cadd(cnt.dark, (u32)(cntb - __popcll(LM)));
             npos += cntb;
-            n_leaf += (u32)cntb;
+            cadd(cnt.leaf, (u32)cntb);
             qhead = qwrap(qhead + cntb);
             qn -= cntb;
             i += cntb;
@@ -1615,7 +1644,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             if (s_n == 0 && SM)
                 s_first = __builtin_amdgcn_readlane(pos, __builtin_ctzll(SM));
             s_n += __popcll(SM);
-            n_slow += (u32)__popcll(SM);
+            cadd(cnt.slow, (u32)__popcll(SM));
             /* overlap-heavy scenes (e.g. a box of sky half-spaces) stop trying */
             if (fast_on && 4 * __popcll(SM) > 3 * cf)
                 fast_on = 0;
@@ -1727,11 +1756,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     }
     f.retval = retval;
     f.i = i;
-    cnt.rounds += n_rounds;
-    cnt.attempts += n_att;
-    cnt.leaf += n_leaf;
-    cnt.slow += n_slow;
-    cnt.dark += n_dark;
     return reason;
 }
 
