@@ -1178,8 +1178,8 @@ struct Counters
 {
     u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow, dark;
 #ifdef PT_PHASE_TIMING
-    u64 ph[7]; /* cycles: generation, stage A, fast pass, slow pass, group sums, burst total, sample total */
-    u64 np[8]; /* events: bursts, loop iterations, stage-A passes, fast passes, slow passes, group sums, fast lanes, slow lanes */
+    u64 ph[7]; /* cycles: generation, (unused), fast pass, slow pass, group sums, burst total, sample total */
+    u64 np[8]; /* events: bursts, loop iterations, (unused), fast passes, slow passes, group sums, fast lanes, slow lanes */
 #define PT_CNT(c, k, v) (c).np[k] += (v)
 #else
 #define PT_CNT(c, k, v)
@@ -1211,12 +1211,10 @@ __device__ __forceinline__ void cadd(u64 &c, u32 v)
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
-    V3 *q;                /* PT_QCAP queued leaf-child directions                         */
+    unsigned char *flags; /* PT_FCAP child positions (mod): 1 = the child holds a ring slot */
     void *ctx;            /* the burst origin's S::Root::Ctx, prepared once per burst     */
     float4 *ring;         /* PT_RCAP kept-child slots: parked ray, then the child's term */
-    u64 *gmask;           /* PT_GCAP groups of 64 children: which lanes hold a ring slot */
-    unsigned char *fastq; /* PT_SCAP slots waiting for the fast pass (position mod 256) */
-    unsigned char *slowq; /* PT_SCAP slots waiting for the full merge                   */
+    unsigned char *slowq; /* PT_SCAP slots waiting for the full merge (ring number mod 256) */
 };
 
 /* ---------------------------------------------------------------- spine --- */
@@ -1245,11 +1243,10 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #ifndef PT_KATT
 #define PT_KATT 4 /* rejection attempts per lane per generation round */
 #endif
-#define PT_QCAP (64 + 64 * PT_KATT) /* leaf-child ring per wave: < 64 queued + 64*PT_KATT accepted per round */
-#define PT_RCAP 256 /* kept-child slots per wave awaiting their group sum          */
-#define PT_GCAP 32  /* groups per wave awaiting their sum                           */
-#define PT_SCAP 256 /* parked children per queue (byte offsets): a drain can add 2 x 64 to < 64 */
-static_assert(64 + 64 * PT_KATT <= PT_QCAP, "queue too small for PT_KATT");
+#define PT_RCAP 256  /* kept-child slots per wave awaiting their group sum            */
+#define PT_FCAP 2048 /* child-position flags per wave (32 groups of 64)               */
+#define PT_SCAP 256  /* parked children awaiting the full merge (<= PT_RCAP, byte ring numbers) */
+static_assert(64 * PT_KATT <= PT_FCAP / 2, "position flags too few for PT_KATT");
 #define PT_JUMP_ENTRIES 321 /* host table: m = 0..320 attempts */
 static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
 
@@ -1373,15 +1370,14 @@ template <class S, bool STRICT, bool DEFERRED, bool KR0>
 __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
-    V3 *const q = L.q;
     float4 *const ring = L.ring;
-    unsigned char *const fastq = L.fastq, *const slowq = L.slowq;
+    unsigned char *const flags = L.flags, *const slowq = L.slowq;
     const int lane = threadIdx.x & 63;
     const u64 below = (1ull << lane) - 1ull;
     const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
     const float sc = unif(f.sc), strength = unif(f.strength), add = unif(f.add);
     const int depth = uni(f.depth), N = uni(f.N);
-    int i = uni(f.i);
+    const int i = uni(f.i);
     V3 retval = univ(f.retval);
     const V3 kR = univ((1.0f / sc - 1.0f) * univ(f.refl)); /* (1 / scatter_coefficient - 1) * reflectedRayDir */
     const float sNa = unif((strength / (float)N) * add);  /* strength / scatter_ray_count * addFactor           */
@@ -1391,47 +1387,49 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const u64 ginc = G3l * rng.inc;
     const u64 A64 = jump[128], g64inc = jump[129] * rng.inc;   /* 64 attempts = 192 draws  */
     const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * rng.inc; /* a full round */
-    int qhead = 0, qn = 0, fails = 0, reason = -1;
-    /* x mod PT_QCAP for 0 <= x < 2 * PT_QCAP */
-    auto qwrap = [](int x) { return (int)min((u32)x, (u32)(x - PT_QCAP)); };
-    /* the burst origin's primitive contexts, shared by every pass of the burst */
+    int fails = 0, reason = -1;
+    /* the burst origin's primitive contexts, shared by every pass of the burst
+     * (and, in registers, by the generation rounds' dark test) */
     typename S::Root::Ctx *const cxp = (typename S::Root::Ctx *)L.ctx;
-    {
-        typename S::Root::Ctx c;
-        S::Root::prep(c, hit, e);
-        *cxp = c;
-    }
-    /* children are numbered in stage-A order (npos); stage A's batches of 64 are
-     * the summation groups.  A DARK child (no emissive primitive reachable, and a
-     * positive weight) has the burst-uniform term Z = rc * 0 and takes no ring
-     * slot; every other child is KEPT in the slot ring (numbered nkeep), and each
-     * group records which of its lanes were kept (gmask). */
-    int npos = 0, f_head = 0, f_n = 0, s_head = 0, s_n = 0;
-    int nkeep = 0, keep_sum = 0, ngrp = 0, gsum = 0;
-    /* register copies of LDS queue heads: ring number of the first entry of
-     * fastq / slowq (valid while non-empty) and the oldest unsummed group's mask */
-    int f_first = 0, s_first = 0;
-    u64 head_gm = 0ull;
-    u64 *const gmask = L.gmask;
+    typename S::Root::Ctx c0;
+    S::Root::prep(c0, hit, e);
+    *cxp = c0;
+    /* Children are numbered by position in the burst (npos); positions 64g ..
+     * 64g + 63 form summation group g (the oracle's GROUP64 groups).  A DARK
+     * child (no emissive primitive reachable, positive weight) has the
+     * burst-uniform term Z = rc * 0: the generation round decides it on the
+     * accepted direction and it takes no memory beyond its position flag.
+     * Every other child is KEPT: the round parks its direction in the slot
+     * ring (numbered nkeep, in position order), where it waits for the fast
+     * pass and, if it fails the check there, the slow pass; flags[position]
+     * records which positions hold a ring slot. */
+    int npos = 0, nkeep = 0, keep_sum = 0, gsum = 0, f_n = 0, s_head = 0, s_n = 0, s_first = 0;
     /* ((aN * factor) * rc) * (+0) == rc * (+0) bitwise for any finite aN * factor > 0 */
     const V3 Z = rc * mk(0.0f, 0.0f, 0.0f);
     int fast_on = 1;
-    /* RAW: stage A decides dark children on the unnormalised direction
-     * (dark_raw, sound but conservative).  Its Z shortcut also needs a factor
-     * >= +0, i.e. a computed dot(normalize(w), n) >= 0: accepted w have a
-     * computed n.w > EPS and |w| <= 1 + |kR| (< 65), so the rounding of
-     * normalize and dot (< 7e-5 here) cannot flip the sign. */
+    /* RAW: dark children are decided on the unnormalised direction (dark_raw,
+     * sound but conservative).  The Z shortcut also needs a factor >= +0, i.e.
+     * a computed dot(normalize(w), n) >= 0: accepted w have a computed
+     * n.w > EPS and |w| <= 1 + |kR| (< 65), so the rounding of normalize and
+     * dot (< 7e-5 here) cannot flip the sign.  Without RAW every child is kept
+     * and the fast pass computes its exact term. */
     constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
     const bool raw_on = KR0 || length(kR) < 64.0f;
+    /* queued slots hold ring numbers mod 256; every pending one lies in
+     * [keep_sum, keep_sum + PT_RCAP), which restores it */
+    auto slot_pos = [&](unsigned char v) { return keep_sum + ((int)(v - keep_sum) & (PT_RCAP - 1)); };
     PT_CNT(cnt, 0, 1);
     for (;;) {
         PT_CNT(cnt, 1, 1);
-        if (reason < 0 && qn < 64) {
+        /* a round needs 64 free ring slots (more kept children than free slots
+         * end the round early, below) and 64*PT_KATT free position flags */
+        const bool room = PT_RCAP - (nkeep - keep_sum) >= 64 && npos - 64 * gsum <= PT_FCAP - 64 * PT_KATT;
+        if (reason < 0 && room) {
             PT_T0(tg);
             PT_MARK(13);
             /* ---- generation round: lane l evaluates attempts l, 64 + l, ... */
             Attempt at[PT_KATT];
-            u64 Am[PT_KATT], Fm[PT_KATT], NLm[PT_KATT];
+            u64 Am[PT_KATT], Fm[PT_KATT], NLm[PT_KATT], Dm[PT_KATT];
             {
                 u64 sk = A3l * rng.st + ginc;
 #pragma unroll
@@ -1442,20 +1440,52 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     Am[k] = at[k].A;
                     Fm[k] = at[k].F;
                     NLm[k] = at[k].NL;
+                    Dm[k] = 0ull;
+                    if (RAW)
+                        Dm[k] = __ballot(raw_on && S::Root::template dark_raw<Emissive<S>>(c0, at[k].wn, e));
                 }
             }
             cadd(cnt.rounds, 1u);
             /* ---- replay the sequential consumption rule on the masks */
-            int rem = N - (i + qn);
-            u64 take[PT_KATT];
+            int rem = N - (i + npos);
+            int free_slots = PT_RCAP - (nkeep - keep_sum);
+#ifdef PT_ROOM_CAP
+            free_slots = min(free_slots, PT_ROOM_CAP); /* test hook: force early round ends */
+#endif
+            u64 take[PT_KATT], keep[PT_KATT];
             int m = 0; /* attempts consumed this round, 1..64*PT_KATT */
+            bool cut = false;
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
                 take[k] = 0ull;
-                if (reason < 0) {
+                keep[k] = 0ull;
+                if (reason < 0 && !cut) {
+                    const int fails_in = fails;
                     const int c = replay(Am[k], Fm[k], NLm[k], rem, fails, reason, take[k]);
                     m = 64 * k + c + 1;
                     rem -= __popcll(Am[k]);
+                    u64 kp = take[k] & ~Dm[k];
+                    if (__popcll(kp) > free_slots) {
+                        /* the slot ring is full: the round ends just before the
+                         * first kept child without a slot (it is drawn again by
+                         * the next round); no stop rule fired before it */
+                        const int pos = nth_set_bit(kp, free_slots + 1);
+                        const u64 pre = (1ull << pos) - 1ull;
+                        take[k] &= pre;
+                        kp &= pre;
+                        const u64 ca = Am[k] & pre;
+                        if (ca) {
+                            const int last = 63 - __builtin_clzll(ca);
+                            fails = __popcll(Fm[k] & pre & ~((2ull << last) - 1ull));
+                        } else {
+                            fails = fails_in + __popcll(Fm[k] & pre);
+                        }
+                        reason = -1;
+                        m = 64 * k + pos;
+                        cut = true;
+                    }
+                    keep[k] = kp;
+                    free_slots -= __popcll(kp);
                 }
             }
             if (!DEFERRED && reason == B_NONLEAF) {
@@ -1476,14 +1506,25 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 child.depth = depth - 1;
             }
             cadd(cnt.attempts, (u32)m);
-            int base = qwrap(qhead + qn);
+            /* ---- position flags for every consumed child, ring slots for the kept */
+            int p = npos, kb = nkeep;
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
-                if ((take[k] >> lane) & 1ull)
-                    q[qwrap(base + __popcll(take[k] & below))] = at[k].wn;
-                base = qwrap(base + __popcll(take[k]));
-                qn += __popcll(take[k]);
+                if ((take[k] >> lane) & 1ull) {
+                    const bool kl = (keep[k] >> lane) & 1ull;
+                    flags[(p + __popcll(take[k] & below)) & (PT_FCAP - 1)] = kl ? 1 : 0;
+                    if (kl)
+                        ring[(kb + __popcll(keep[k] & below)) & (PT_RCAP - 1)] =
+                            make_float4(at[k].wn.x, at[k].wn.y, at[k].wn.z, at[k].factor);
+                }
+                p += __popcll(take[k]);
+                kb += __popcll(keep[k]);
             }
+            cadd(cnt.leaf, (u32)(p - npos));
+            cadd(cnt.dark, (u32)((p - npos) - (kb - nkeep)));
+            f_n += kb - nkeep;
+            npos = p;
+            nkeep = kb;
             /* ---- advance the sample's stream past the consumed attempts */
             if (m == 64 * PT_KATT)
                 rng.st = Afull * rng.st + gfullinc;
@@ -1492,172 +1533,82 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             PT_ACC(cnt, 0, tg);
             PT_MARK(15);
         }
-        if (qn >= 64 || (reason >= 0 && qn > 0)) {
-            PT_T0(ta);
-            PT_MARK(14);
-            /* ---- stage A: one queued leaf child per lane.  A child whose ray no
-             * emissive primitive meets at t >= eps has the term weight * (+0)
-             * whatever the CSG makes of it (merges only copy primitive
-             * boundaries, and the scan qualifies a boundary only at t >= eps):
-             * it finishes here.  The others park their ray in the slot ring and
-             * queue for the fast pass. */
-            const int cntb = qn < 64 ? qn : 64;
-            PT_CNT(cnt, 2, 1);
-            int lit = 0, keep = 0;
-            float4 out = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (RAW) {
-                /* every child here is a leaf: the raw test alone decides dark;
-                 * kept children park their unnormalised direction and the fast
-                 * pass normalises them, 64 useful lanes at a time */
-                if (lane < cntb) {
-                    const V3 w = q[qwrap(qhead + lane)];
-                    const typename S::Root::Ctx ctx = *cxp;
-                    keep = !(raw_on && S::Root::template dark_raw<Emissive<S>>(ctx, w, e));
-                    lit = keep;
-                    out = make_float4(w.x, w.y, w.z, 0.0f);
-                }
-            } else if (lane < cntb) {
-                V3 dir = q[qwrap(qhead + lane)];
-                if (DEFERRED)
-                    dir = cnormalize(dir);
-                /* the factor of path-trace.h:160, the same expression as at
-                 * generation in the non-deferred case */
-                float4 en;
-                en.w = 1.0f - (1.0f - dot(dir, n)) * sc;
-#if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 1
-                /* experiment: generation cost only */
-                {
-                    const V3 col = dir.z < 0.0f ? S::emis(0, hit + dir, e) : mk(0, 0, 0);
-                    const V3 term = ((aN * en.w) * rc) * col;
-                    out = make_float4(term.x, term.y, term.z, 0.0f);
-                    keep = 1;
-                }
-#else
-                {
-                    const typename S::Root::Ctx ctx = *cxp;
-                    PrimSpans<S::Root::HI> ps;
-                    S::Root::template span_sel<Emissive<S>>(ps, ctx, mkray(dir), e);
-                    S::Root::template each_sel<Emissive<S>>([&](auto x) {
-                        constexpr int X = decltype(x)::value;
-                        lit |= ps.live[X] & (ps.t1[X] >= EPS);
-                    });
-                }
-                if (lit) {
-                    out = make_float4(dir.x, dir.y, dir.z, en.w);
-                    keep = 1;
-                } else if (!(en.w > 0.0f)) {
-                    /* not provably Z: keep the exact term */
-                    const V3 term = ((aN * en.w) * rc) * mk(0.0f, 0.0f, 0.0f);
-                    out = make_float4(term.x, term.y, term.z, 0.0f);
-                    keep = 1;
-                }
-#endif
-            }
-            const u64 KM = __ballot(keep), LM = __ballot(lit);
-            const int kidx = nkeep + __popcll(KM & below);
-            if (keep)
-                ring[kidx & (PT_RCAP - 1)] = out;
-            if (lit)
-                fastq[(f_head + f_n + __popcll(LM & below)) & (PT_SCAP - 1)] = (unsigned char)kidx;
-            if (lane == 0)
-                gmask[ngrp & (PT_GCAP - 1)] = KM;
-            if (gsum == ngrp)
-                head_gm = KM;
-            if (f_n == 0 && LM)
-                f_first = nkeep + __popcll(KM & ((1ull << __builtin_ctzll(LM)) - 1ull));
-            ngrp++;
-            nkeep += __popcll(KM);
-            f_n += __popcll(LM);
-            cadd(cnt.dark, (u32)(cntb - __popcll(LM)));
-            npos += cntb;
-            cadd(cnt.leaf, (u32)cntb);
-            qhead = qwrap(qhead + cntb);
-            qn -= cntb;
-            i += cntb;
-            PT_ACC(cnt, 1, ta);
-            PT_MARK(15);
-        }
-        const bool final = reason >= 0 && qn == 0;
-        /* queued slots hold ring numbers mod 256; every pending one lies in
-         * [keep_sum, keep_sum + PT_RCAP), which restores it */
-        auto slot_pos = [&](unsigned char v) { return keep_sum + ((int)(v - keep_sum) & (PT_RCAP - 1)); };
-        /* drain everything when the next stage-A batch might not fit */
-        const bool pressure = nkeep - keep_sum > PT_RCAP - 64 || ngrp - gsum > PT_GCAP - 2;
+        const bool final = reason >= 0;
+        /* drain everything when the next round would not fit */
+        const bool drain =
+            final || PT_RCAP - (nkeep - keep_sum) < 64 || npos - 64 * gsum > PT_FCAP - 64 * PT_KATT;
         PT_T0(tb);
-        /* ---- stage B: fast pass over 64 parked children.  Lanes whose spans
-         * pass the fast check finish; the others stay parked for the full merge */
-        while (f_n > 0 && (f_n >= 64 || final || pressure)) {
+        /* ---- fast pass over the next 64 kept children (ring order).  Lanes
+         * whose spans pass the fast check finish; the others stay parked for
+         * the full merge */
+        while (f_n > 0 && (f_n >= 64 || drain)) {
             const int cf = f_n < 64 ? f_n : 64;
+            const int pos0 = nkeep - f_n;
+            const int pos = pos0 + lane;
             PT_CNT(cnt, 3, 1);
             PT_CNT(cnt, 6, cf);
-            int slow = 0, pos = 0;
-            if (lane < cf && !fast_on) {
-                /* the fast check keeps failing in this burst: park for the full merge */
-                pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
-                slow = 1;
-                if (RAW) {
-                    const float4 en = ring[pos & (PT_RCAP - 1)];
-                    const V3 dir = cnormalize(mk(en.x, en.y, en.z));
-                    ring[pos & (PT_RCAP - 1)] = make_float4(dir.x, dir.y, dir.z, 1.0f - (1.0f - dot(dir, n)) * sc);
-                }
-            } else if (lane < cf) {
-                pos = slot_pos(fastq[(f_head + lane) & (PT_SCAP - 1)]);
+            int slow = 0;
+            if (lane < cf) {
                 float4 en = ring[pos & (PT_RCAP - 1)];
-                if (RAW) {
-                    /* the normalisation and factor stage A left to this pass
-                     * (the same expressions as path-trace.h:157, :160) */
+                if (DEFERRED) {
+                    /* the normalisation and factor of path-trace.h:157, :160,
+                     * left to this pass so that 64 useful lanes do them */
                     const V3 nd = cnormalize(mk(en.x, en.y, en.z));
                     en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
                 }
-                const V3 dir = mk(en.x, en.y, en.z);
-                PT_MARK(8);
-                const typename S::Root::Ctx ctx = *cxp;
-                PrimSpans<S::Root::HI> ps;
-                PT_MARK(9);
-                S::Root::span(ps, ctx, mkray(dir), e);
-                PT_MARK(10);
-                const int fok = S::Root::fast_ok(ps);
-                PT_MARK(11);
-                if (fok) {
-                    float t = 0.0f;
-                    int mat = 0;
-                    V3 col = mk(0, 0, 0);
-                    if (fast_first_hit<typename S::Root>(ps, t, mat))
-                        col = S::emis(mat, hit + t * dir, e);
-                    PT_MARK(12);
-                    const V3 term = ((aN * en.w) * rc) * col;
-                    ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
-                } else {
-#if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 3
-                    /* experiment: no slow passes (slow lanes contribute 0) */
-                    ring[pos & (PT_RCAP - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#else
+                if (!fast_on) {
+                    /* the fast check keeps failing in this burst: park for the full merge */
                     slow = 1;
-                    if (RAW)
+                    if (DEFERRED)
                         ring[pos & (PT_RCAP - 1)] = en;
+                } else {
+                    const V3 dir = mk(en.x, en.y, en.z);
+                    PT_MARK(8);
+                    const typename S::Root::Ctx ctx = *cxp;
+                    PrimSpans<S::Root::HI> ps;
+                    PT_MARK(9);
+                    S::Root::span(ps, ctx, mkray(dir), e);
+                    PT_MARK(10);
+                    const int fok = S::Root::fast_ok(ps);
+                    PT_MARK(11);
+                    if (fok) {
+                        float t = 0.0f;
+                        int mat = 0;
+                        V3 col = mk(0, 0, 0);
+                        if (fast_first_hit<typename S::Root>(ps, t, mat))
+                            col = S::emis(mat, hit + t * dir, e);
+                        PT_MARK(12);
+                        const V3 term = ((aN * en.w) * rc) * col;
+                        ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
+                    } else {
+#if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 3
+                        /* experiment: no slow passes (slow lanes contribute 0) */
+                        ring[pos & (PT_RCAP - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#else
+                        slow = 1;
+                        if (DEFERRED)
+                            ring[pos & (PT_RCAP - 1)] = en;
 #endif
+                    }
                 }
             }
             const u64 SM = __ballot(slow);
             if (slow)
                 slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = (unsigned char)pos;
             if (s_n == 0 && SM)
-                s_first = __builtin_amdgcn_readlane(pos, __builtin_ctzll(SM));
+                s_first = pos0 + __builtin_ctzll(SM);
             s_n += __popcll(SM);
             cadd(cnt.slow, (u32)__popcll(SM));
             /* overlap-heavy scenes (e.g. a box of sky half-spaces) stop trying */
             if (fast_on && 4 * __popcll(SM) > 3 * cf)
                 fast_on = 0;
-            f_head += cf;
             f_n -= cf;
-            if (f_n)
-                f_first = slot_pos(uni(fastq[f_head & (PT_SCAP - 1)]));
         }
         PT_ACC(cnt, 2, tb);
         PT_T0(tc);
         /* ---- stage C: slow passes, 64 parked children at a time through the
          * full merge */
-        while (s_n > 0 && (s_n >= 64 || final || pressure)) {
+        while (s_n > 0 && (s_n >= 64 || drain)) {
             const int cs = s_n < 64 ? s_n : 64;
             PT_CNT(cnt, 4, 1);
             PT_CNT(cnt, 7, cs);
@@ -1684,22 +1635,19 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
         PT_T0(ts);
         /* ---- sum finished groups in order: 64 children per group (the last
          * group of a burst may be shorter), group-64 tree or sequential; a
-         * group is finished when every kept child in it has its term */
+         * group is finished when all its positions are consumed and every
+         * kept child in it has its term */
         {
-            int resolved = nkeep;
+            int resolved = nkeep - f_n;
             if (s_n)
-                resolved = s_first;
-            if (f_n)
-                resolved = min(resolved, f_first);
+                resolved = min(resolved, s_first);
+            const int ngrp = final ? (npos + 63) >> 6 : npos >> 6;
             while (gsum < ngrp) {
-                const u64 gm = head_gm;
+                const int cg = min(64, npos - 64 * gsum);
+                const u64 gm = __ballot(lane < cg && flags[(64 * gsum + lane) & (PT_FCAP - 1)]);
                 const int gk = __popcll(gm);
                 if (keep_sum + gk > resolved)
                     break;
-                u64 nx = 0ull;
-                if (gsum + 1 < ngrp)
-                    nx = gmask[(gsum + 1) & (PT_GCAP - 1)];
-                const int cg = min(64, npos - 64 * gsum);
                 PT_CNT(cnt, 5, 1);
                 V3 term = mk(-0.0f, -0.0f, -0.0f);
                 if (lane < cg)
@@ -1710,16 +1658,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 }
                 if (!STRICT && gsum + 1 < ngrp) {
                     /* groups finish in batches (a slow pass resolves many at
-                     * once): when the next group is finished too, its six
+                     * once): when the next group is finished too, its three
                      * tree sums run interleaved with these; retval still adds
                      * the group sums one after the other */
-                    const u64 gm2 = ((u64)(u32)uni((int)(nx >> 32)) << 32) | (u64)(u32)uni((int)nx);
+                    const int cg2 = min(64, npos - 64 * (gsum + 1));
+                    const u64 gm2 = __ballot(lane < cg2 && flags[(64 * (gsum + 1) + lane) & (PT_FCAP - 1)]);
                     const int gk2 = __popcll(gm2);
                     if (keep_sum + gk + gk2 <= resolved) {
-                        u64 nx2 = 0ull;
-                        if (gsum + 2 < ngrp)
-                            nx2 = gmask[(gsum + 2) & (PT_GCAP - 1)];
-                        const int cg2 = min(64, npos - 64 * (gsum + 1));
                         PT_CNT(cnt, 5, 1);
                         V3 term2 = mk(-0.0f, -0.0f, -0.0f);
                         if (lane < cg2)
@@ -1734,7 +1679,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         retval = univ(retval + g2);
                         keep_sum += gk + gk2;
                         gsum += 2;
-                        head_gm = ((u64)(u32)uni((int)(nx2 >> 32)) << 32) | (u64)(u32)uni((int)nx2);
                         continue;
                     }
                 }
@@ -1747,7 +1691,6 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 }
                 keep_sum += gk;
                 gsum++;
-                head_gm = ((u64)(u32)uni((int)(nx >> 32)) << 32) | (u64)(u32)uni((int)nx);
             }
         }
         PT_ACC(cnt, 4, ts);
@@ -1755,7 +1698,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             break;
     }
     f.retval = retval;
-    f.i = i;
+    f.i = i + npos;
     return reason;
 }
 
@@ -2038,11 +1981,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                                              const PtLaunch &lp)
 {
     __shared__ Frame stk[PT_WPW][MAXD + 1];
-    __shared__ V3 qbuf[PT_WPW][PT_QCAP];
+    __shared__ unsigned char pbuf[PT_WPW][PT_FCAP];
     __shared__ typename S::Root::Ctx xbuf[PT_WPW];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
-    __shared__ u64 gbuf[PT_WPW][PT_GCAP];
-    __shared__ unsigned char fbuf[PT_WPW][PT_SCAP];
     __shared__ unsigned char sbuf[PT_WPW][PT_SCAP];
     __shared__ Counters cbuf[PT_WPW];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2056,7 +1997,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
 #endif
-    const WaveLds L = {qbuf[wave], &xbuf[wave], rbuf[wave], gbuf[wave], fbuf[wave], sbuf[wave]};
+    const WaveLds L = {pbuf[wave], &xbuf[wave], rbuf[wave], sbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
