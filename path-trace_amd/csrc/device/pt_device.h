@@ -43,6 +43,7 @@ namespace ptd
 constexpr float EPS = 1e-3f;      /* include/misc.h:7 */
 constexpr float MAXV = 1e20f;     /* include/misc.h:8 */
 constexpr u64 LCG_MULT = 214013ull; /* DefaultRandomEngine, include/path-trace.h:47 */
+constexpr u64 LCG_INC = 2531011ull;  /* include/path-trace.h:47 */
 
 /* -------------------------------------------------------------- launch --- */
 struct PtImage
@@ -281,12 +282,26 @@ __device__ __forceinline__ void rng_seed(Rng &r, u64 seed, u64 pixel, u64 sample
 {
     u64 key = splitmix64(seed) ^ (pixel << 20) ^ sample;
     r.st = splitmix64(key);
-    r.inc = 2531011ull;
+    r.inc = LCG_INC;
 }
 __device__ __forceinline__ u32 rng_next(Rng &r)
 {
     r.st = r.st * LCG_MULT + r.inc;
     return lcg_out(r.st);
+}
+/* One engine step on the state's 32-bit words: (lo * M + inc) gives the new
+ * low word and a carry below 2^19; hi * M + carry gives the new high word
+ * (the output).  Two 32x32->64 multiply-adds instead of a generic 64-bit
+ * multiply; the same state mod 2^64. */
+struct W2
+{
+    u32 lo, hi;
+};
+__device__ __forceinline__ W2 lcg_step(W2 s)
+{
+    const u64 t = (u64)s.lo * LCG_MULT + LCG_INC;
+    const u32 hi = (u32)((u64)s.hi * LCG_MULT + (t >> 32));
+    return {(u32)t, hi};
 }
 /* uniform_real_distribution<float>, vector3d.h:22-33, for (0,1) and (-1,1) */
 __device__ __forceinline__ float u01(u32 o) { return (float)o / 4294967296.0f; }
@@ -303,6 +318,8 @@ __device__ __forceinline__ float rdlane(float v, int l)
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 __device__ __forceinline__ V3 univ(V3 v) { return mk(unif(v.x), unif(v.y), unif(v.z)); }
+/* all-ones if the wave-uniform p holds, else 0, by scalar arithmetic */
+__device__ __forceinline__ u64 uni_mask(bool p) { return 0ull - (u64)(u32)uni(p ? 1 : 0); }
 __device__ __forceinline__ int nth_set_bit(u64 m, int k) /* 1-based k, m has >= k bits */
 {
     for (int j = 1; j < k; j++)
@@ -522,7 +539,7 @@ struct Sph
         return normalize((o + t * d) - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
     /* Sound test on an UNNORMALISED direction w that the span of normalize(w)
-     * is dead or ends before EPS (stage A of the scatter loop).  Origin
+     * is dead or ends before EPS (the generation round's dark test).  Origin
      * outside (c > 0) and receding (b > 0): disc = fl(fl(b*b) - a*c) <= fl(b*b),
      * so sqrt(disc) <= b and t1 = (-b + sqrt(disc)) / a <= 0.  b's sign is
      * read off B = omc.w with a margin (1e-6 of sum |omc_i w_i|) that covers
@@ -531,17 +548,22 @@ struct Sph
     __device__ static constexpr bool raw_ok() { return true; }
     template <class SEL>
     __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
+    /* The test as a wave mask, one ballot per compare (a ballot of a combined
+     * predicate is lowered through a v_cndmask / v_cmp round trip) */
     template <class SEL>
-    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &)
+    __device__ static __forceinline__ u64 dark_mask(const Ctx &c, V3 w, const Env &)
     {
         if constexpr (!SEL::take(MAT))
-            return true;
+            return ~0ull;
         const float B = dot(c.omc, w);
         const float s = (__builtin_fabsf(c.omc.x * w.x) + __builtin_fabsf(c.omc.y * w.y)) +
                         __builtin_fabsf(c.omc.z * w.z);
         const bool pre = c.c > 0.0f && (__builtin_fabsf(c.omc.x) + __builtin_fabsf(c.omc.y)) +
                                                __builtin_fabsf(c.omc.z) < 1e15f;
-        return pre && B > __builtin_fmaxf(1e-6f * s, 1e-30f);
+        /* pre is wave-uniform: a scalar mask, neither a ballot of pre && x
+         * (InstCombine folds ballot(a) & ballot(b) into that) nor a branch
+         * (which would split the round's interleaved attempts) */
+        return __ballot(B > __builtin_fmaxf(1e-6f * s, 1e-30f)) & uni_mask(pre);
     }
 };
 
@@ -621,7 +643,7 @@ struct Pln
     {
         return normalize(mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
-    /* Sound dark test on an unnormalised direction w (see Sph::dark_raw).
+    /* Sound dark test on an unnormalised direction w (see Sph::dark_mask).
      * With num <= -1e-6 the span of normalize(w) is dead or ends before EPS
      * unless div = n.normalize(w) <= -1e-6: div in (-1e-6, 1e-6) is
      * degenerate (dead), div >= 1e-6 gives t1 = num / div < 0 (or |t| >= 1e20,
@@ -632,14 +654,14 @@ struct Pln
     template <class SEL>
     __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
     template <class SEL>
-    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &e)
+    __device__ static __forceinline__ u64 dark_mask(const Ctx &c, V3 w, const Env &e)
     {
         if constexpr (!SEL::take(MAT))
-            return true;
+            return ~0ull;
         const V3 np = mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
         const bool pre = c.num <= -(EPS * EPS) &&
                          (__builtin_fabsf(np.x) + __builtin_fabsf(np.y)) + __builtin_fabsf(np.z) <= 1.5f;
-        return pre && dot(w, np) >= 0.0f;
+        return __ballot(dot(w, np) >= 0.0f) & uni_mask(pre);
     }
 };
 
@@ -713,9 +735,9 @@ struct Pln
     template <class SEL>                                                                            \
     __device__ static constexpr int nsel() { return A::template nsel<SEL>() + B::template nsel<SEL>(); } \
     template <class SEL>                                                                            \
-    __device__ static __forceinline__ bool dark_raw(const Ctx &c, V3 w, const Env &e)              \
+    __device__ static __forceinline__ u64 dark_mask(const Ctx &c, V3 w, const Env &e)              \
     {                                                                                               \
-        return A::template dark_raw<SEL>(c.a, w, e) & B::template dark_raw<SEL>(c.b, w, e);         \
+        return A::template dark_mask<SEL>(c.a, w, e) & B::template dark_mask<SEL>(c.b, w, e);       \
     }
 
 /* Each merge step decides what to emit and which child to advance, then
@@ -900,7 +922,7 @@ struct Xf
     template <class SEL>
     __device__ static constexpr int nsel() { return C::template nsel<SEL>(); }
     template <class SEL>
-    __device__ static __forceinline__ bool dark_raw(const Ctx &, V3, const Env &) { return true; }
+    __device__ static __forceinline__ u64 dark_mask(const Ctx &, V3, const Env &) { return ~0ull; }
 };
 
 /* First qualifying span of the root, traceRay's scan (path-trace.h:66-100). */
@@ -1241,13 +1263,13 @@ struct Frame
 enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 
 #ifndef PT_KATT
-#define PT_KATT 4 /* rejection attempts per lane per generation round */
+#define PT_KATT 8 /* rejection attempts per lane per generation round (A/B on C3: 4 -> 8 +6%) */
 #endif
 #define PT_RCAP 256  /* kept-child slots per wave awaiting their group sum            */
 #define PT_FCAP 2048 /* child-position flags per wave (32 groups of 64)               */
 #define PT_SCAP 256  /* parked children awaiting the full merge (<= PT_RCAP, byte ring numbers) */
 static_assert(64 * PT_KATT <= PT_FCAP / 2, "position flags too few for PT_KATT");
-#define PT_JUMP_ENTRIES 321 /* host table: m = 0..320 attempts */
+#define PT_JUMP_ENTRIES 1025 /* host table: m = 0..1024 attempts */
 static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
 
 /* One rejection attempt of the scatter loop body (path-trace.h:141-158):
@@ -1265,10 +1287,9 @@ template <bool DEFERRED, bool KR0>
 __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float sc, float sNa, float abs_rc,
                                            bool child_leaf_depth)
 {
-    const u64 s1 = s0 * LCG_MULT + inc;
-    const u64 s2 = s1 * LCG_MULT + inc;
-    const u64 s3 = s2 * LCG_MULT + inc;
-    const V3 v = mk(u11(lcg_out(s1)), u11(lcg_out(s2)), u11(lcg_out(s3)));
+    (void)inc; /* the engine's increment, LCG_INC */
+    const W2 s1 = lcg_step({(u32)s0, (u32)(s0 >> 32)}), s2 = lcg_step(s1), s3 = lcg_step(s2);
+    const V3 v = mk(u11(s1.hi), u11(s2.hi), u11(s3.hi));
     /* rand(): while (mag > max) with mag = sqrt(|v|^2); correctly rounded
      * sqrt(x) > 1  <=>  x > 1 + 2^-23 (exhaustively checked) */
     const bool ball = !(dot(v, v) > 0x1.000002p+0f);
@@ -1407,14 +1428,14 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     /* ((aN * factor) * rc) * (+0) == rc * (+0) bitwise for any finite aN * factor > 0 */
     const V3 Z = rc * mk(0.0f, 0.0f, 0.0f);
     int fast_on = 1;
-    /* RAW: dark children are decided on the unnormalised direction (dark_raw,
+    /* RAW: dark children are decided on the unnormalised direction (dark_mask,
      * sound but conservative).  The Z shortcut also needs a factor >= +0, i.e.
      * a computed dot(normalize(w), n) >= 0: accepted w have a computed
      * n.w > EPS and |w| <= 1 + |kR| (< 65), so the rounding of normalize and
      * dot (< 7e-5 here) cannot flip the sign.  Without RAW every child is kept
      * and the fast pass computes its exact term. */
     constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
-    const bool raw_on = KR0 || length(kR) < 64.0f;
+    const u64 raw_mask = uni_mask(KR0 || length(kR) < 64.0f);
     /* queued slots hold ring numbers mod 256; every pending one lies in
      * [keep_sum, keep_sum + PT_RCAP), which restores it */
     auto slot_pos = [&](unsigned char v) { return keep_sum + ((int)(v - keep_sum) & (PT_RCAP - 1)); };
@@ -1442,7 +1463,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     NLm[k] = at[k].NL;
                     Dm[k] = 0ull;
                     if (RAW)
-                        Dm[k] = __ballot(raw_on && S::Root::template dark_raw<Emissive<S>>(c0, at[k].wn, e));
+                        Dm[k] = S::Root::template dark_mask<Emissive<S>>(c0, at[k].wn, e) & raw_mask;
                 }
             }
             cadd(cnt.rounds, 1u);

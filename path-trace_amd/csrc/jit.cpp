@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <iterator>
 #include <mutex>
 #include <sstream>
 
@@ -80,7 +81,21 @@ const char *kOptions[] = {
     "-fhip-fp32-correctly-rounded-divide-sqrt",    /* IEEE-exact f32 '/' and sqrt                           */
     "-fno-gpu-flush-denormals-to-zero",           /* keep f32 denormals as the reference does              */
     "-fno-fast-math",
+    "-fno-slp-vectorize", /* packing pairs of f32 ops into v_pk_* costs more v_mov than it saves (A/B on C3) */
 };
+
+/* experiment hook: extra compiler options, e.g. PT_JIT_OPTIONS="-fno-slp-vectorize" */
+std::vector<std::string> extra_options()
+{
+    std::vector<std::string> v;
+    if (const char *env = getenv("PT_JIT_OPTIONS")) {
+        std::istringstream in(env);
+        std::string o;
+        while (in >> o)
+            v.push_back(o);
+    }
+    return v;
+}
 
 std::string cache_dir()
 {
@@ -104,6 +119,7 @@ std::string full_key(const Generated &g)
     std::ostringstream k;
     k << g.source << "\n";
     for (const char *o : kOptions) k << o << "\n";
+    for (const std::string &o : extra_options()) k << o << "\n";
     k << "hiprtc " << maj << "." << min << "\n";
     uint64_t h = 1469598103934665603ull;
     for (unsigned char c : k.str()) {
@@ -124,8 +140,11 @@ std::vector<char> compile(const Generated &g, std::string &log)
     hiprtcProgram prog;
     if (R.create(&prog, g.source.c_str(), "pt_scene.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         throw Error(PT_ERR_COMPILE, "hiprtcCreateProgram failed");
-    int n = (int)(sizeof(kOptions) / sizeof(kOptions[0]));
-    hiprtcResult r = R.compile(prog, n, kOptions);
+    std::vector<const char *> opts(std::begin(kOptions), std::end(kOptions));
+    const std::vector<std::string> extra = extra_options();
+    for (const std::string &o : extra)
+        opts.push_back(o.c_str());
+    hiprtcResult r = R.compile(prog, (int)opts.size(), opts.data());
     size_t ls = 0;
     R.log_size(prog, &ls);
     log.assign(ls, '\0');

@@ -404,12 +404,13 @@ void load_text(SceneImpl &s, const std::string &text)
     s.root = root;
 }
 
-/* jump table (A_{3m}, G_{3m}), m = 0..320 (PT_KATT <= 5), of state_{n+3m} = A*state_n + G*inc
- * (PT_JUMP_ENTRIES of the device code: up to 5 x 64 attempts per round) */
+/* jump table (A_{3m}, G_{3m}), m = 0..1024 (PT_KATT <= 16), of state_{n+3m} = A*state_n + G*inc
+ * (PT_JUMP_ENTRIES of the device code: up to 16 x 64 attempts per round) */
 std::vector<uint64_t> jump_table()
 {
-    std::vector<uint64_t> t(2 * 321);
-    for (uint32_t m = 0; m <= 320; m++) pt_lcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
+    constexpr uint32_t kEntries = 1025;
+    std::vector<uint64_t> t(2 * kEntries);
+    for (uint32_t m = 0; m < kEntries; m++) pt_lcg_jump_coeffs(3 * m, &t[2 * m], &t[2 * m + 1]);
     return t;
 }
 
