@@ -14,6 +14,7 @@
 #include <sstream>
 #include <vector>
 
+#include <cmath>
 #include "internal.h"
 
 namespace pt
@@ -82,7 +83,16 @@ struct Gen
         }
         case ObjKind::Plane: {
             int off = put(o.f, 4);
-            t << "Pln<" << prim++ << "," << off << "," << material(o.mat) << ">";
+            /* axis-aligned normal: lets the scatter loop's dark test be a sign test */
+            int ax = -1, nz = 0;
+            for (int k = 0; k < 3; k++)
+                if (o.f[k] != 0.0f) {
+                    nz++;
+                    ax = 2 * k + (o.f[k] < 0.0f ? 1 : 0);
+                }
+            if (nz != 1 || !std::isfinite(o.f[ax >> 1]))
+                ax = -1;
+            t << "Pln<" << prim++ << "," << off << "," << material(o.mat) << "," << ax << ">";
             planes++;
             break;
         }

@@ -568,7 +568,12 @@ struct Sph
 };
 
 /* Plane half-space {p : n.p + d < 0} (src/plane.cpp:35-63).  P[OFF..] = n, d. */
-template <int PRIM, int OFF, int MAT>
+#ifndef PT_PLANE_AXIS_DARK
+#define PT_PLANE_AXIS_DARK 1
+#endif
+/* AX >= 0: the normal has one nonzero component, axis AX >> 1, negative if
+ * AX & 1 (codegen knows the scene's numbers); -1 otherwise. */
+template <int PRIM, int OFF, int MAT, int AX = -1>
 struct Pln
 {
     static constexpr int LO = PRIM, HI = PRIM + 1;
@@ -661,6 +666,12 @@ struct Pln
         const V3 np = mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
         const bool pre = c.num <= -(EPS * EPS) &&
                          (__builtin_fabsf(np.x) + __builtin_fabsf(np.y)) + __builtin_fabsf(np.z) <= 1.5f;
+        if constexpr (AX >= 0 && PT_PLANE_AXIS_DARK) {
+            /* the exact n.w is n_a * w_a: its sign test is one compare (the
+             * bound above holds for an exact n.w >= 0 as for a computed one) */
+            const float wa = (AX >> 1) == 0 ? w.x : (AX >> 1) == 1 ? w.y : w.z;
+            return __ballot((AX & 1) ? wa <= 0.0f : wa >= 0.0f) & uni_mask(pre);
+        }
         return __ballot(dot(w, np) >= 0.0f) & uni_mask(pre);
     }
 };

@@ -569,6 +569,8 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
          * trace many samples of one expensive pixel while others idle */
         const long long waves = (long long)ds.resident_blocks * ds.wpw;
         int chunk = 16;
+        if (const char *env = getenv("PT_CHUNK_MAX")) /* experiment hook (1..64) */
+            chunk = std::max(1, std::min(64, atoi(env)));
         while (chunk > 1 && n_items / chunk < 4 * waves) chunk /= 2;
         long long chunks = (n_items + chunk - 1) / chunk;
         const int wpw = ds.wpw;
