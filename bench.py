@@ -56,30 +56,60 @@ def parse():
     ap.add_argument("--warmup", type=int, default=0)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override (for quick local probes only; invalid metric)")
-    ap.add_argument("--cpu-pixels", type=int, default=512)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-pixels", type=int, default=2048)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS "
+                         "when set (the GPU box exports its per-GPU CPU share there)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--order", default="fast")
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, txt, spp, npix, threads):
-    """The reference's own hot path on host cores over a hashed pixel subset."""
+def cpu_threads(requested: int) -> int:
+    """Host threads for the CPU baseline: the CPUs this process may use, capped
+    by OMP_NUM_THREADS (the GPU box's per-GPU CPU share) when that is set."""
+    if requested > 0:
+        return requested
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps):
+    """The reference's own hot path (tracePixel per (pixel, sample), src/test.cpp:450;
+    one std::thread per host core as RenderBlock's pool, src/test.cpp:204) over a
+    hashed pixel subset of the same frame.  Per-sample cost is bimodal (sky vs
+    diffuse pixels), so the subset's queries/sample is reported beside the
+    frame's and the rate is also given rescaled by their ratio (CPU time is
+    proportional to span queries)."""
     import oracle_py as O
     rng = np.random.default_rng(0x5EED)
     pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
+    qps = None
     if O.ref_available():
         kind = "reference"
         res, info = O.ref_render(txt, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, pixels=pix,
                                  threads=threads, info=True)
         secs = info["seconds"]
+        qps = info["queries"] / (npix * spp)
     else:  # restated oracle (same arithmetic, pinned to the reference by tests/golden)
         kind = "port"
         t0 = time.time()
-        res = O.render(txt, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, pixels=pix, threads=threads)
+        res, st = O.render(txt, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, pixels=pix,
+                           threads=threads, stats=True)
         secs = time.time() - t0
-    return pix, res, {"value": npix * spp / secs / 1e6, "unit": "Msamples/s", "cores": threads, "kind": kind,
-                      "sample": "%d hashed pixels x %d spp of the same frame (%.1f s)" % (npix, spp, secs)}
+        qps = st["queries"] / (npix * spp)
+    value = npix * spp / secs / 1e6
+    out = {"value": round(value, 5), "unit": "Msamples/s", "cores": threads, "kind": kind,
+           "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+           "sample": "%d hashed pixels x %d spp of the same frame (%.1f s)" % (npix, spp, secs),
+           "sample_queries_per_sample": round(qps, 2)}
+    if frame_qps:
+        out["frame_queries_per_sample"] = round(frame_qps, 2)
+        out["value_rescaled_to_frame"] = round(value * qps / frame_qps, 5)
+    return pix, res, out
 
 
 def main():
@@ -171,7 +201,7 @@ def main():
         if not args.no_cpu and world == 1:
             try:
                 pix, ref, cb = cpu_baseline(cfg, to_text(root, "/tmp/pt_bench_img"), spp, args.cpu_pixels,
-                                            args.cpu_threads)
+                                            cpu_threads(args.cpu_threads), queries / samples)
                 gpu = frame.reshape(-1, 3)[pix]
                 out["rmse_vs_cpu_ref"] = [float(v) for v in
                                           np.sqrt(np.mean((gpu.astype(np.float64) - ref) ** 2, axis=0))]

@@ -138,11 +138,14 @@ typedef struct pt_render_stats {
     uint64_t samples;              /* traceRay calls from tracePixel                            */
     uint64_t queries;              /* root span queries (spine + leaf children)                 */
     uint64_t leaf_queries;         /* of which wave-cooperative leaf children                   */
-    uint64_t attempts;             /* rejection attempts evaluated (64 per round)               */
+    uint64_t attempts;             /* rejection attempts consumed (a round evaluates 512)       */
     uint64_t rounds;               /* attempt rounds                                            */
     uint64_t sphere_tests, sphere_hits, plane_tests;
     uint64_t slow_queries;         /* leaf children that needed the full CSG merge (slow pass)  */
     uint64_t dark_queries;         /* leaf children no emissive primitive can light: weight * 0 */
+    uint64_t mid_queries;          /* leaf children the clear pass could not finish (fast check) */
+    double wave_ms;                /* mean render-wave lifetime (device clock); kernel_ms minus
+                                      this is the launch's tail, where waves have run out of work */
 } pt_render_stats;
 
 /* Synchronous: renders the frame into rgb_out (host memory), which receives,

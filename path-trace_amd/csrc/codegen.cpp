@@ -221,6 +221,14 @@ Generated generate(const SceneImpl &s, int depth)
 
     std::ostringstream src;
     /* experiment hook: extra preprocessor definitions, e.g. PT_DEVICE_DEFINES="PT_LEAF_STUB=1" */
+    static const bool announce = [] {
+        for (const char *h : {"PT_DEVICE_DEFINES", "PT_DEVICE_HEADER"})
+            if (const char *v = getenv(h))
+                if (*v)
+                    fprintf(stderr, "pt: experiment hook %s=\"%s\" active\n", h, v);
+        return true;
+    }();
+    (void)announce;
     if (const char *defs = getenv("PT_DEVICE_DEFINES")) {
         std::istringstream ds(defs);
         std::string d;

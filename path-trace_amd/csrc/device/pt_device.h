@@ -9,18 +9,23 @@
  * trees.  All per-scene control flow is therefore static and every node's
  * state lives in VGPRs; scene constants are scalar loads from P.
  *
- * Execution model (one 64-lane wavefront = one workgroup):
- *   - a wave owns a chunk of 64 consecutive (pixel, sample) items and traces
- *     them one after another; the ray tree of one sample is walked by all 64
+ * Execution model (PT_WPW independent 64-lane waves per workgroup, each with
+ * its own LDS work areas):
+ *   - a wave dequeues a chunk of up to PT_CHUNK consecutive (pixel, sample)
+ *     items; lane j traces item j's camera query and finishes the sample
+ *     itself when its tree is that query plus at most one leaf mirror child
+ *     (lane_sample); the other items are walked one after another by all 64
  *     lanes together with wave-uniform state (the "spine": camera ray, mirror
  *     and refraction chains, non-leaf children) and an explicit frame stack in
  *     LDS instead of the reference's recursion (include/path-trace.h:58-165);
  *   - a scatter loop with scatter_coefficient > eps (path-trace.h:138-163) is a
- *     BURST: the wave evaluates 64 rejection attempts at once, lane l jumping
- *     the engine stream 3*l draws ahead (O(1) LCG jump), ballots accept / fail /
- *     non-leaf masks, replays the reference's sequential consumption rule with
- *     scalar bit arithmetic, queues accepted leaf children in LDS and traces
- *     them 64 at a time, one child per lane;
+ *     BURST: each generation round evaluates 64*PT_KATT consecutive rejection
+ *     attempts, PT_KATT per lane (attempt l + 64k, its stream position reached
+ *     by O(1) LCG jumps), ballots accept / fail / non-leaf / dark masks,
+ *     replays the reference's sequential consumption rule with scalar bit
+ *     arithmetic, parks the accepted children that may be lit in an LDS ring
+ *     and traces them 64 at a time, one child per lane, through a cascade of
+ *     compacted passes (clear, fast, full merge);
  *   - a leaf child (depth-1 <= 0 or child strength < eps: path-trace.h:105-108)
  *     draws no random numbers, so children of a burst are independent and
  *     the RNG stream and every branch stay bit-identical to the reference.
@@ -268,7 +273,7 @@ __device__ __forceinline__ V3 m_lin(const float *__restrict__ m, V3 v)
  * starting state -- include/pt/pt_engine.h is the specification. */
 struct Rng
 {
-    u64 st, inc;
+    u64 st; /* the increment is always LCG_INC (pt_engine.h) */
 };
 __device__ __forceinline__ u64 splitmix64(u64 x)
 {
@@ -282,11 +287,10 @@ __device__ __forceinline__ void rng_seed(Rng &r, u64 seed, u64 pixel, u64 sample
 {
     u64 key = splitmix64(seed) ^ (pixel << 20) ^ sample;
     r.st = splitmix64(key);
-    r.inc = LCG_INC;
 }
 __device__ __forceinline__ u32 rng_next(Rng &r)
 {
-    r.st = r.st * LCG_MULT + r.inc;
+    r.st = r.st * LCG_MULT + LCG_INC;
     return lcg_out(r.st);
 }
 /* One engine step on the state's 32-bit words: (lo * M + inc) gives the new
@@ -320,6 +324,14 @@ __device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin
 __device__ __forceinline__ V3 univ(V3 v) { return mk(unif(v.x), unif(v.y), unif(v.z)); }
 /* all-ones if the wave-uniform p holds, else 0, by scalar arithmetic */
 __device__ __forceinline__ u64 uni_mask(bool p) { return 0ull - (u64)(u32)uni(p ? 1 : 0); }
+/* base + set bits of the uniform mask m in the lanes below this one (v_mbcnt) */
+__device__ __forceinline__ int mbcnt(u64 m, int base)
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, (u32)base));
+}
+/* this lane's bit of the uniform mask m (the JIT runs on the clang that torch
+ * bundles, which has no __builtin_amdgcn_inverse_ballot_w64) */
+__device__ __forceinline__ bool lane_in(u64 m) { return (m >> (threadIdx.x & 63)) & 1ull; }
 __device__ __forceinline__ int nth_set_bit(u64 m, int k) /* 1-based k, m has >= k bits */
 {
     for (int j = 1; j < k; j++)
@@ -467,22 +479,38 @@ struct Sph
     {
         V3 omc;
         float c;
+        float thr; /* clear_mask's bound on b for a normalised direction */
     };
     struct St
     {
         float t0, t1;
         int live; /* int, not bool: kept in a VGPR instead of an SGPR lane mask */
     };
+    /* clear_mask: for a direction d with |d|^2 = a in 1 +- 2^-20 the span ends
+     * before EPS whenever b = (o - c).d >= thr:
+     *  - c > 0 (origin outside), thr = 0: fl(a*c) >= 0 makes disc <= fl(b*b),
+     *    so sqrt(disc) <= sqrt(fl(b*b)) = b and t1 = (-b + sqrt(disc)) / a <= 0;
+     *  - c <= 0 (origin on or inside: the burst origin's own sphere), thr =
+     *    527 |c| and b <= r <= 99: -b + sqrt(disc) is exact (Sterbenz) and at
+     *    most (2u + u^2) b + (1 + u)^2 a |c| / (2b), so t1 <= 2u b / a +
+     *    (1 + 3u) |c| / (2b) < 1.2e-5 + 9.5e-4 < EPS (u = 2^-24).
+     * NaN c gives a NaN threshold: never clear. */
+    __device__ static __forceinline__ float clear_thr(float c, const Env &e)
+    {
+        return c > 0.0f ? 0.0f : e.P[OFF + 3] < 9801.0f ? -c * 527.0f : __builtin_inff();
+    }
     __device__ static __forceinline__ void prep(Ctx &c, V3 o, const Env &e)
     {
         c.omc = univ(o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
         c.c = unif(dot(c.omc, c.omc) - e.P[OFF + 3]);
+        c.thr = unif(clear_thr(c.c, e));
     }
     /* the same for a per-lane origin */
     __device__ static __forceinline__ void prep_l(Ctx &c, V3 o, const Env &e)
     {
         c.omc = o - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
         c.c = dot(c.omc, c.omc) - e.P[OFF + 3];
+        c.thr = clear_thr(c.c, e);
     }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &)
     {
@@ -530,8 +558,22 @@ struct Sph
     __device__ static __forceinline__ void each_sel(F &&f)
     {
         if constexpr (SEL::take(MAT))
-            f(IC<PRIM>());
+            f(IC<PRIM>(), IC<MAT>());
     }
+    /* Lanes whose span is dead or provably ends before EPS (unselected
+     * primitives only; NORM: q.d is a normalised direction, see clear_thr) */
+    template <class SEL, bool NORM>
+    __device__ static __forceinline__ u64 clear_mask(const Ctx &c, const Ray &q, const Env &)
+    {
+        if constexpr (SEL::take(MAT))
+            return ~0ull;
+        const float b = dot(c.omc, q.d);
+        const float disc = b * b - q.a * c.c;
+        const float thr = NORM ? c.thr : (c.c > 0.0f ? 0.0f : __builtin_inff());
+        return __ballot(disc <= EPS) | __ballot(b >= thr);
+    }
+    template <class SEL>
+    __device__ static constexpr bool clear_ok() { return true; }
     template <class PS>
     __device__ static __forceinline__ int fast_ok(const PS &) { return 1; }
     __device__ static __forceinline__ V3 normal(int, float t, V3 o, V3 d, const Env &e)
@@ -640,8 +682,19 @@ struct Pln
     __device__ static __forceinline__ void each_sel(F &&f)
     {
         if constexpr (SEL::take(MAT))
-            f(IC<PRIM>());
+            f(IC<PRIM>(), IC<MAT>());
     }
+    template <class SEL, bool NORM>
+    __device__ static __forceinline__ u64 clear_mask(const Ctx &c, const Ray &q, const Env &e)
+    {
+        if constexpr (SEL::take(MAT))
+            return ~0ull;
+        St s;
+        init(s, c, q, e);
+        return __ballot(!s.live) | __ballot(s.t1 < EPS);
+    }
+    template <class SEL>
+    __device__ static constexpr bool clear_ok() { return true; }
     template <class PS>
     __device__ static __forceinline__ int fast_ok(const PS &) { return 1; }
     __device__ static __forceinline__ V3 normal(int, float, V3, V3, const Env &e)
@@ -728,6 +781,11 @@ struct Pln
         A::template each_sel<SEL>(f);                                                               \
         B::template each_sel<SEL>(f);                                                               \
     }                                                                                               \
+    template <class SEL, bool NORM>                                                                 \
+    __device__ static __forceinline__ u64 clear_mask(const Ctx &c, const Ray &q, const Env &e)     \
+    {                                                                                               \
+        return A::template clear_mask<SEL, NORM>(c.a, q, e) & B::template clear_mask<SEL, NORM>(c.b, q, e); \
+    }                                                                                               \
     template <class PS>                                                                             \
     __device__ static __forceinline__ int fast_ok(const PS &ps)                                     \
     {                                                                                               \
@@ -761,6 +819,8 @@ struct Uni
 {
     static constexpr int KIND = NODE_UNION;
     PTD_BINARY_COMMON
+    template <class SEL>
+    __device__ static constexpr bool clear_ok() { return A::template clear_ok<SEL>() && B::template clear_ok<SEL>(); }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f)
     {
@@ -806,6 +866,8 @@ struct Isect
 {
     static constexpr int KIND = NODE_ISECT;
     PTD_BINARY_COMMON
+    template <class SEL>
+    __device__ static constexpr bool clear_ok() { return A::template nsel<SEL>() + B::template nsel<SEL>() == 0; }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&) {}
     __device__ static __forceinline__ bool pull(St &s, CS &out)
@@ -847,6 +909,8 @@ struct Diff
 {
     static constexpr int KIND = NODE_DIFF;
     PTD_BINARY_COMMON
+    template <class SEL>
+    __device__ static constexpr bool clear_ok() { return A::template nsel<SEL>() + B::template nsel<SEL>() == 0; }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { A::each_pos(f); }
     __device__ static __forceinline__ bool pull(St &s, CS &out)
@@ -920,6 +984,15 @@ struct Xf
     }
     template <class SEL, class F>
     __device__ static __forceinline__ void each_sel(F &&f) { C::template each_sel<SEL>(f); }
+    /* the transformed direction is not normalised: spheres inside use the
+     * origin-outside rule only */
+    template <class SEL, bool NORM>
+    __device__ static __forceinline__ u64 clear_mask(const Ctx &c, const Ray &q, const Env &e)
+    {
+        return C::template clear_mask<SEL, false>(c.c, mkray(m_lin(e.P + MOFF, q.d)), e);
+    }
+    template <class SEL>
+    __device__ static constexpr bool clear_ok() { return C::template clear_ok<SEL>(); }
     template <class PS>
     __device__ static __forceinline__ int fast_ok(const PS &ps) { return C::fast_ok(ps); }
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)
@@ -968,6 +1041,61 @@ __device__ __forceinline__ bool fast_first_hit(const PS &ps, float &t, int &mat)
     int found = 0, bm = 0;
     float b0 = 0.0f, b1 = 0.0f;
     R::each_pos([&](auto x, auto m) {
+        constexpr int X = decltype(x)::value;
+        const int cand = ps.live[X] & (ps.t1[X] >= EPS);
+        const int better = cand & ((!found) | (ps.t0[X] < b0));
+        b0 = better ? ps.t0[X] : b0;
+        b1 = better ? ps.t1[X] : b1;
+        bm = better ? decltype(m)::value : bm;
+        found |= cand;
+    });
+    mat = bm;
+    if (!found || b0 >= MAXV)
+        return false;
+    if (b0 >= EPS) {
+        t = b0;
+        return true;
+    }
+    if (b1 >= MAXV)
+        return false;
+    t = b1;
+    return true;
+}
+
+/* ---- clear pass -------------------------------------
+ * When every selected (emissive) primitive is reached from the root through
+ * Union and TransformedObject nodes only (R::clear_ok), and on a lane every
+ * other primitive's span is dead or ends before EPS (R::clear_mask), the
+ * lazy merges cannot move the first qualifying span away from the selected
+ * primitives' own: a Difference or Intersection subtree then holds no
+ * selected primitive, so each span it emits starts and ends at boundaries of
+ * its own spans (src/difference.cpp:84-135, src/intersection.cpp:84-130,
+ * including the :124-130 quirk's inverted spans) and ends before EPS; at a
+ * Union (src/union.cpp:84-134) such a span either lies strictly before a
+ * selected span that starts at >= EPS, or merges with one that starts before
+ * EPS into a span starting before EPS and ending at that span's own end (the
+ * larger end, with its normal) -- the scan (path-trace.h:66-100) skips the
+ * former and stops at that same end in the latter.  So the first hit is
+ * fast_first_hit over the selected primitives alone, checked pairwise like
+ * the fast pass (pair_ok at a Union) when there are several. */
+template <class R, class SEL, class PS>
+__device__ __forceinline__ int sel_pairs_ok(const PS &ps)
+{
+    int ok = 1;
+    R::template each_sel<SEL>([&](auto x, auto) {
+        R::template each_sel<SEL>([&](auto y, auto) {
+            if constexpr (decltype(x)::value < decltype(y)::value)
+                ok &= pair_ok<NODE_UNION>(ps, decltype(x)::value, decltype(y)::value);
+        });
+    });
+    return ok;
+}
+template <class R, class SEL, class PS>
+__device__ __forceinline__ bool sel_first_hit(const PS &ps, float &t, int &mat)
+{
+    int found = 0, bm = 0;
+    float b0 = 0.0f, b1 = 0.0f;
+    R::template each_sel<SEL>([&](auto x, auto m) {
         constexpr int X = decltype(x)::value;
         const int cand = ps.live[X] & (ps.t1[X] >= EPS);
         const int better = cand & ((!found) | (ps.t0[X] < b0));
@@ -1209,9 +1337,9 @@ struct TSpherical
 /* Per-wave statistics, kept in LDS (every lane writes the same value). */
 struct Counters
 {
-    u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow, dark;
+    u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow, dark, mid;
 #ifdef PT_PHASE_TIMING
-    u64 ph[7]; /* cycles: generation, (unused), fast pass, slow pass, group sums, burst total, sample total */
+    u64 ph[7]; /* cycles: generation, its attempts, fast pass, slow pass, group sums, burst total, sample total */
     u64 np[8]; /* events: bursts, loop iterations, (unused), fast passes, slow passes, group sums, fast lanes, slow lanes */
 #define PT_CNT(c, k, v) (c).np[k] += (v)
 #else
@@ -1248,6 +1376,7 @@ struct WaveLds
     void *ctx;            /* the burst origin's S::Root::Ctx, prepared once per burst     */
     float4 *ring;         /* PT_RCAP kept-child slots: parked ray, then the child's term */
     unsigned char *slowq; /* PT_SCAP slots waiting for the full merge (ring number mod 256) */
+    unsigned char *midq;  /* PT_SCAP slots the clear pass could not finish (fast check next) */
 };
 
 /* ---------------------------------------------------------------- spine --- */
@@ -1278,7 +1407,7 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #endif
 #define PT_RCAP 256  /* kept-child slots per wave awaiting their group sum            */
 #define PT_FCAP 2048 /* child-position flags per wave (32 groups of 64)               */
-#define PT_SCAP 256  /* parked children awaiting the full merge (<= PT_RCAP, byte ring numbers) */
+#define PT_SCAP 128  /* mid / slow queue entries (< 128 pending by construction; byte ring numbers) */
 static_assert(64 * PT_KATT <= PT_FCAP / 2, "position flags too few for PT_KATT");
 #define PT_JUMP_ENTRIES 1025 /* host table: m = 0..1024 attempts */
 static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
@@ -1295,10 +1424,9 @@ struct Attempt
 /* The predicates are balloted where they are produced, so they never pass
  * through a per-lane integer. */
 template <bool DEFERRED, bool KR0>
-__device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float sc, float sNa, float abs_rc,
+__device__ __forceinline__ Attempt attempt(u64 s0, V3 n, V3 kR, float sc, float sNa, float abs_rc,
                                            bool child_leaf_depth)
 {
-    (void)inc; /* the engine's increment, LCG_INC */
     const W2 s1 = lcg_step({(u32)s0, (u32)(s0 >> 32)}), s2 = lcg_step(s1), s3 = lcg_step(s2);
     const V3 v = mk(u11(s1.hi), u11(s2.hi), u11(s3.hi));
     /* rand(): while (mag > max) with mag = sqrt(|v|^2); correctly rounded
@@ -1311,6 +1439,22 @@ __device__ __forceinline__ Attempt attempt(u64 s0, u64 inc, V3 n, V3 kR, float s
     Attempt a;
     /* one ballot per compare (a ballot of a combined predicate is lowered
      * through a v_cndmask / v_cmp round trip) */
+#ifdef PT_PAD_VALU /* experiment: extra independent VALU work per attempt */
+    {
+        float pad = v.x;
+        for (int i = 0; i < PT_PAD_VALU; i++)
+            asm volatile("v_add_f32 %0, %0, %0" : "+v"(pad));
+        asm volatile("" ::"v"(pad));
+    }
+#endif
+#ifdef PT_PAD_SALU /* experiment: extra SALU work per attempt */
+    {
+        int pad = 0;
+        for (int i = 0; i < PT_PAD_SALU; i++)
+            asm volatile("s_add_u32 %0, %0, 1" : "+s"(pad));
+        asm volatile("" ::"s"(pad));
+    }
+#endif
     const u64 BB = __ballot(ball), HB = __ballot(hemi);
     a.A = BB & HB;
     a.F = BB & ~HB;
@@ -1403,7 +1547,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
     float4 *const ring = L.ring;
-    unsigned char *const flags = L.flags, *const slowq = L.slowq;
+    unsigned char *const flags = L.flags, *const slowq = L.slowq, *const midq = L.midq;
     const int lane = threadIdx.x & 63;
     const u64 below = (1ull << lane) - 1ull;
     const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
@@ -1416,9 +1560,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const float aN = unif(add / (float)N);                /* addFactor / scatter_ray_count                       */
     const float abs_rc = unif(length(rc));
     const bool child_leaf_depth = depth - 1 <= 0;
-    const u64 ginc = G3l * rng.inc;
-    const u64 A64 = jump[128], g64inc = jump[129] * rng.inc;   /* 64 attempts = 192 draws  */
-    const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * rng.inc; /* a full round */
+    const u64 ginc = G3l * LCG_INC;
+    const u64 A64 = jump[128], g64inc = jump[129] * LCG_INC;   /* 64 attempts = 192 draws  */
+    const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * LCG_INC; /* a full round */
     int fails = 0, reason = -1;
     /* the burst origin's primitive contexts, shared by every pass of the burst
      * (and, in registers, by the generation rounds' dark test) */
@@ -1436,9 +1580,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
      * pass and, if it fails the check there, the slow pass; flags[position]
      * records which positions hold a ring slot. */
     int npos = 0, nkeep = 0, keep_sum = 0, gsum = 0, f_n = 0, s_head = 0, s_n = 0, s_first = 0;
+    int m_head = 0, m_n = 0, m_first = 0;
     /* ((aN * factor) * rc) * (+0) == rc * (+0) bitwise for any finite aN * factor > 0 */
     const V3 Z = rc * mk(0.0f, 0.0f, 0.0f);
-    int fast_on = 1;
+    int fast_on = 1, clear_on = 1;
+    /* the clear pass applies when every emissive primitive hangs off the root
+     * through Unions and transforms only */
+    constexpr bool CLEAR = S::Root::template clear_ok<Emissive<S>>();
     /* RAW: dark children are decided on the unnormalised direction (dark_mask,
      * sound but conservative).  The Z shortcut also needs a factor >= +0, i.e.
      * a computed dot(normalize(w), n) >= 0: accepted w have a computed
@@ -1468,7 +1616,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 for (int k = 0; k < PT_KATT; k++) {
                     if (k)
                         sk = A64 * sk + g64inc;
-                    at[k] = attempt<DEFERRED, KR0>(sk, rng.inc, n, kR, sc, sNa, abs_rc, child_leaf_depth);
+                    at[k] = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
                     Am[k] = at[k].A;
                     Fm[k] = at[k].F;
                     NLm[k] = at[k].NL;
@@ -1477,6 +1625,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         Dm[k] = S::Root::template dark_mask<Emissive<S>>(c0, at[k].wn, e) & raw_mask;
                 }
             }
+            PT_ACC(cnt, 1, tg); /* the attempts alone (slot 1) */
             cadd(cnt.rounds, 1u);
             /* ---- replay the sequential consumption rule on the masks */
             int rem = N - (i + npos);
@@ -1487,6 +1636,35 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             u64 take[PT_KATT], keep[PT_KATT];
             int m = 0; /* attempts consumed this round, 1..64*PT_KATT */
             bool cut = false;
+            /* Common case: the whole round is consumed -- fewer accepted
+             * children than remain, no non-leaf child, a slot for every kept
+             * child, and no abort possible (fails <= 487 and at most 512
+             * failures this round) -- so every half takes all its accepted
+             * attempts, and the consecutive-failure count afterwards is that
+             * of the last half, which has an accepted attempt. */
+            int pa[PT_KATT], pk[PT_KATT];
+            int ta = 0, tk = 0;
+            u64 nlor = 0ull;
+#pragma unroll
+            for (int k = 0; k < PT_KATT; k++) {
+                pa[k] = __popcll(Am[k]);
+                pk[k] = __popcll(Am[k] & ~Dm[k]);
+                ta += pa[k];
+                tk += pk[k];
+                nlor |= NLm[k];
+            }
+            const bool whole = nlor == 0ull && ta < rem && tk <= free_slots && fails <= 487 && Am[PT_KATT - 1] != 0ull;
+            if (whole) {
+#pragma unroll
+                for (int k = 0; k < PT_KATT; k++) {
+                    take[k] = Am[k];
+                    keep[k] = Am[k] & ~Dm[k];
+                }
+                const int last = 63 - __builtin_clzll(Am[PT_KATT - 1]);
+                fails = (last == 63) ? 0 : __popcll(Fm[PT_KATT - 1] >> (last + 1));
+                m = 64 * PT_KATT;
+            }
+            if (!whole) {
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
                 take[k] = 0ull;
@@ -1519,6 +1697,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     keep[k] = kp;
                     free_slots -= __popcll(kp);
                 }
+                pa[k] = __popcll(take[k]);
+                pk[k] = __popcll(keep[k]);
+            }
             }
             if (!DEFERRED && reason == B_NONLEAF) {
                 const int l = (m - 1) & 63, kk = (m - 1) >> 6;
@@ -1542,15 +1723,15 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             int p = npos, kb = nkeep;
 #pragma unroll
             for (int k = 0; k < PT_KATT; k++) {
-                if ((take[k] >> lane) & 1ull) {
-                    const bool kl = (keep[k] >> lane) & 1ull;
-                    flags[(p + __popcll(take[k] & below)) & (PT_FCAP - 1)] = kl ? 1 : 0;
+                if (lane_in(take[k])) {
+                    const bool kl = lane_in(keep[k]);
+                    flags[mbcnt(take[k], p) & (PT_FCAP - 1)] = kl ? 1 : 0;
                     if (kl)
-                        ring[(kb + __popcll(keep[k] & below)) & (PT_RCAP - 1)] =
+                        ring[mbcnt(keep[k], kb) & (PT_RCAP - 1)] =
                             make_float4(at[k].wn.x, at[k].wn.y, at[k].wn.z, at[k].factor);
                 }
-                p += __popcll(take[k]);
-                kb += __popcll(keep[k]);
+                p += pa[k];
+                kb += pk[k];
             }
             cadd(cnt.leaf, (u32)(p - npos));
             cadd(cnt.dark, (u32)((p - npos) - (kb - nkeep)));
@@ -1561,7 +1742,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             if (m == 64 * PT_KATT)
                 rng.st = Afull * rng.st + gfullinc;
             else
-                rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * rng.inc;
+                rng.st = jump[2 * m] * rng.st + jump[2 * m + 1] * LCG_INC;
             PT_ACC(cnt, 0, tg);
             PT_MARK(15);
         }
@@ -1569,101 +1750,178 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
         /* drain everything when the next round would not fit */
         const bool drain =
             final || PT_RCAP - (nkeep - keep_sum) < 64 || npos - 64 * gsum > PT_FCAP - 64 * PT_KATT;
-        PT_T0(tb);
-        /* ---- fast pass over the next 64 kept children (ring order).  Lanes
-         * whose spans pass the fast check finish; the others stay parked for
-         * the full merge */
-        while (f_n > 0 && (f_n >= 64 || drain)) {
-            const int cf = f_n < 64 ? f_n : 64;
-            const int pos0 = nkeep - f_n;
-            const int pos = pos0 + lane;
-            PT_CNT(cnt, 3, 1);
-            PT_CNT(cnt, 6, cf);
-            int slow = 0;
-            if (lane < cf) {
-                float4 en = ring[pos & (PT_RCAP - 1)];
-                if (DEFERRED) {
-                    /* the normalisation and factor of path-trace.h:157, :160,
-                     * left to this pass so that 64 useful lanes do them */
-                    const V3 nd = cnormalize(mk(en.x, en.y, en.z));
-                    en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
-                }
-                if (!fast_on) {
-                    /* the fast check keeps failing in this burst: park for the full merge */
-                    slow = 1;
-                    if (DEFERRED)
-                        ring[pos & (PT_RCAP - 1)] = en;
-                } else {
-                    const V3 dir = mk(en.x, en.y, en.z);
-                    PT_MARK(8);
-                    const typename S::Root::Ctx ctx = *cxp;
-                    PrimSpans<S::Root::HI> ps;
-                    PT_MARK(9);
-                    S::Root::span(ps, ctx, mkray(dir), e);
-                    PT_MARK(10);
-                    const int fok = S::Root::fast_ok(ps);
-                    PT_MARK(11);
-                    if (fok) {
-                        float t = 0.0f;
-                        int mat = 0;
-                        V3 col = mk(0, 0, 0);
-                        if (fast_first_hit<typename S::Root>(ps, t, mat))
-                            col = S::emis(mat, hit + t * dir, e);
-                        PT_MARK(12);
-                        const V3 term = ((aN * en.w) * rc) * col;
-                        ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
-                    } else {
-#if defined(PT_LEAF_STUB) && PT_LEAF_STUB == 3
-                        /* experiment: no slow passes (slow lanes contribute 0) */
-                        ring[pos & (PT_RCAP - 1)] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#else
-                        slow = 1;
-                        if (DEFERRED)
-                            ring[pos & (PT_RCAP - 1)] = en;
-#endif
-                    }
-                }
-            }
-            const u64 SM = __ballot(slow);
-            if (slow)
-                slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = (unsigned char)pos;
-            if (s_n == 0 && SM)
-                s_first = pos0 + __builtin_ctzll(SM);
-            s_n += __popcll(SM);
-            cadd(cnt.slow, (u32)__popcll(SM));
-            /* overlap-heavy scenes (e.g. a box of sky half-spaces) stop trying */
-            if (fast_on && 4 * __popcll(SM) > 3 * cf)
-                fast_on = 0;
-            f_n -= cf;
-        }
-        PT_ACC(cnt, 2, tb);
-        PT_T0(tc);
-        /* ---- stage C: slow passes, 64 parked children at a time through the
-         * full merge */
-        while (s_n > 0 && (s_n >= 64 || drain)) {
-            const int cs = s_n < 64 ? s_n : 64;
-            PT_CNT(cnt, 4, 1);
-            PT_CNT(cnt, 7, cs);
-            if (lane < cs) {
-                const int pos = slot_pos(slowq[(s_head + lane) & (PT_SCAP - 1)]);
-                const float4 en = ring[pos & (PT_RCAP - 1)];
-                const V3 dir = mk(en.x, en.y, en.z);
-                const typename S::Root::Ctx ctx = *cxp;
-                float t;
-                u32 ref;
-                bool ex;
+        /* The fast check of one kept child (its normalised direction and
+         * factor in en): true when its term is written to the ring, false
+         * when it needs the full merge. */
+        auto fast_lane = [&](int pos, float4 en) -> bool {
+            const V3 dir = mk(en.x, en.y, en.z);
+            PT_MARK(8);
+            const typename S::Root::Ctx ctx = *cxp;
+            PrimSpans<S::Root::HI> ps;
+            PT_MARK(9);
+            S::Root::span(ps, ctx, mkray(dir), e);
+            PT_MARK(10);
+            const int fok = S::Root::fast_ok(ps);
+            PT_MARK(11);
+            if (fok) {
+                float t = 0.0f;
+                int mat = 0;
                 V3 col = mk(0, 0, 0);
-                if (first_hit<typename S::Root>(ctx, dir, e, t, ref, ex))
-                    col = S::emis(ref_mat(ref), hit + t * dir, e);
+                if (fast_first_hit<typename S::Root>(ps, t, mat))
+                    col = S::emis(mat, hit + t * dir, e);
+                PT_MARK(12);
                 const V3 term = ((aN * en.w) * rc) * col;
                 ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
+                return true;
             }
-            s_head += cs;
-            s_n -= cs;
-            if (s_n)
-                s_first = slot_pos(uni(slowq[s_head & (PT_SCAP - 1)]));
+            return false;
+        };
+        /* Appends the lanes of SM (positions pos0 + lane, ring order) to a
+         * queue of ring numbers. */
+        auto enqueue = [&](unsigned char *q, int head, int &qn, int &qfirst, u64 SM, int pos0, int pos) {
+            if ((SM >> lane) & 1ull)
+                q[(head + qn + __popcll(SM & below)) & (PT_SCAP - 1)] = (unsigned char)pos;
+            if (qn == 0 && SM)
+                qfirst = pos0 + __builtin_ctzll(SM);
+            qn += __popcll(SM);
+        };
+        /* The passes below run as one scheduler: a queue is served as soon as
+         * it holds 64 entries (partial batches only when draining and nothing
+         * upstream is left), so the mid and slow queues never exceed 127
+         * entries (PT_SCAP). */
+        for (;;) {
+            /* ---- stage C: slow passes, 64 parked children at a time through the
+             * full merge */
+            if (s_n > 0 && (s_n >= 64 || (drain && m_n == 0 && f_n == 0))) {
+                PT_T0(tc);
+                const int cs = s_n < 64 ? s_n : 64;
+                PT_CNT(cnt, 4, 1);
+                PT_CNT(cnt, 7, cs);
+                if (lane < cs) {
+                    const int pos = slot_pos(slowq[(s_head + lane) & (PT_SCAP - 1)]);
+                    const float4 en = ring[pos & (PT_RCAP - 1)];
+                    const V3 dir = mk(en.x, en.y, en.z);
+                    const typename S::Root::Ctx ctx = *cxp;
+                    float t;
+                    u32 ref;
+                    bool ex;
+                    V3 col = mk(0, 0, 0);
+                    if (first_hit<typename S::Root>(ctx, dir, e, t, ref, ex))
+                        col = S::emis(ref_mat(ref), hit + t * dir, e);
+                    const V3 term = ((aN * en.w) * rc) * col;
+                    ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
+                }
+                s_head += cs;
+                s_n -= cs;
+                if (s_n)
+                    s_first = slot_pos(uni(slowq[s_head & (PT_SCAP - 1)]));
+                PT_ACC(cnt, 3, tc);
+                continue;
+            }
+            /* ---- fast check on 64 children of the mid queue at a time (CLEAR
+             * scenes); failing lanes go on to the full merge.  The mid queue is in
+             * ring order, so the slow queue it feeds stays in ring order. */
+            if (CLEAR && m_n > 0 && (m_n >= 64 || (drain && f_n == 0))) {
+                PT_T0(tb);
+                const int cm = m_n < 64 ? m_n : 64;
+                int slow = 0, pos = 0;
+                if (lane < cm) {
+                    pos = slot_pos(midq[(m_head + lane) & (PT_SCAP - 1)]);
+                    const float4 en = ring[pos & (PT_RCAP - 1)];
+                    slow = (!fast_on || !fast_lane(pos, en)) ? 1 : 0;
+                }
+                const u64 SM = __ballot(slow);
+                const int p0 = uni(__builtin_amdgcn_readlane(pos, SM ? __builtin_ctzll(SM) : 0));
+                if ((SM >> lane) & 1ull)
+                    slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = (unsigned char)pos;
+                if (s_n == 0 && SM)
+                    s_first = p0;
+                s_n += __popcll(SM);
+                cadd(cnt.slow, (u32)__popcll(SM));
+                if (fast_on && 4 * __popcll(SM) > 3 * cm)
+                    fast_on = 0;
+                m_head += cm;
+                m_n -= cm;
+                if (m_n)
+                    m_first = slot_pos(uni(midq[m_head & (PT_SCAP - 1)]));
+                PT_ACC(cnt, 2, tb);
+                continue;
+            }
+            /* ---- first pass over the next 64 kept children (ring order).  With
+             * CLEAR, lanes on which every non-emissive primitive is dead or ends
+             * before EPS finish on the emissive primitives alone (about 4 in 5 of
+             * C3's lit children); the others go to the mid queue for the fast
+             * check.  Without CLEAR this is the fast check itself. */
+            if (f_n > 0 && (f_n >= 64 || drain)) {
+                PT_T0(tb);
+                const int cf = f_n < 64 ? f_n : 64;
+                const int pos0 = nkeep - f_n;
+                const int pos = pos0 + lane;
+                PT_CNT(cnt, 3, 1);
+                PT_CNT(cnt, 6, cf);
+                int park = 0; /* 1: mid queue, 2: slow queue */
+                if (lane < cf) {
+                    float4 en = ring[pos & (PT_RCAP - 1)];
+                    if (DEFERRED) {
+                        /* the normalisation and factor of path-trace.h:157, :160,
+                         * left to this pass so that 64 useful lanes do them */
+                        const V3 nd = cnormalize(mk(en.x, en.y, en.z));
+                        en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
+                    }
+                    if constexpr (CLEAR) {
+                        park = 1;
+                        if (clear_on) {
+                            PT_MARK(16);
+                            const V3 dir = mk(en.x, en.y, en.z);
+                            const typename S::Root::Ctx ctx = *cxp;
+                            const Ray q = mkray(dir);
+                            const u64 CM = S::Root::template clear_mask<Emissive<S>, true>(ctx, q, e);
+                            PrimSpans<S::Root::HI> ps;
+                            S::Root::template span_sel<Emissive<S>>(ps, ctx, q, e);
+                            if (((CM >> lane) & 1ull) && sel_pairs_ok<typename S::Root, Emissive<S>>(ps)) {
+                                float t = 0.0f;
+                                int mat = 0;
+                                V3 col = mk(0, 0, 0);
+                                if (sel_first_hit<typename S::Root, Emissive<S>>(ps, t, mat))
+                                    col = S::emis(mat, hit + t * dir, e);
+                                const V3 term = ((aN * en.w) * rc) * col;
+                                ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
+                                park = 0;
+                            }
+                            PT_MARK(17);
+                        }
+                        if (DEFERRED && park)
+                            ring[pos & (PT_RCAP - 1)] = en;
+                    } else {
+                        if (!fast_on || !fast_lane(pos, en)) {
+                            /* park for the full merge */
+                            park = 2;
+                            if (DEFERRED)
+                                ring[pos & (PT_RCAP - 1)] = en;
+                        }
+                    }
+                }
+                if constexpr (CLEAR) {
+                    const u64 MM = __ballot(park == 1);
+                    enqueue(midq, m_head, m_n, m_first, MM, pos0, pos);
+                    cadd(cnt.mid, (u32)__popcll(MM));
+                    /* the clear test keeps failing in this burst: stop trying */
+                    if (clear_on && 4 * __popcll(MM) > 3 * cf)
+                        clear_on = 0;
+                } else {
+                    const u64 SM = __ballot(park == 2);
+                    enqueue(slowq, s_head, s_n, s_first, SM, pos0, pos);
+                    cadd(cnt.slow, (u32)__popcll(SM));
+                    /* overlap-heavy scenes (e.g. a box of sky half-spaces) stop trying */
+                    if (fast_on && 4 * __popcll(SM) > 3 * cf)
+                        fast_on = 0;
+                }
+                f_n -= cf;
+                PT_ACC(cnt, 2, tb);
+                continue;
+            }
+            break;
         }
-        PT_ACC(cnt, 3, tc);
         PT_T0(ts);
         /* ---- sum finished groups in order: 64 children per group (the last
          * group of a burst may be shorter), group-64 tree or sequential; a
@@ -1671,6 +1929,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
          * kept child in it has its term */
         {
             int resolved = nkeep - f_n;
+            if (m_n)
+                resolved = min(resolved, m_first);
             if (s_n)
                 resolved = min(resolved, s_first);
             const int ngrp = final ? (npos + 63) >> 6 : npos >> 6;
@@ -2017,19 +2277,22 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     __shared__ typename S::Root::Ctx xbuf[PT_WPW];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
     __shared__ unsigned char sbuf[PT_WPW][PT_SCAP];
+    __shared__ unsigned char mbuf[PT_WPW][PT_SCAP];
     __shared__ Counters cbuf[PT_WPW];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const u64 t_start = __builtin_amdgcn_s_memrealtime(); /* 100 MHz: wave lifetimes, stats[26..29] */
     const Env e = {P, imgs};
     const u64 A3l = jump[2 * lane], G3l = jump[2 * lane + 1];
     Counters &cnt = cbuf[wave];
     cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = cnt.slow = cnt.dark = 0;
+    cnt.mid = 0;
 #ifdef PT_PHASE_TIMING
     for (int k = 0; k < 7; k++)
         cnt.ph[k] = 0;
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
 #endif
-    const WaveLds L = {pbuf[wave], &xbuf[wave], rbuf[wave], sbuf[wave]};
+    const WaveLds L = {pbuf[wave], &xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
@@ -2101,6 +2364,12 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         atomicAdd(&stats[5], cnt.nonleaf);
         atomicAdd(&stats[6], cnt.slow);
         atomicAdd(&stats[7], cnt.dark);
+        atomicAdd(&stats[24], cnt.mid);
+        const u64 t_end = __builtin_amdgcn_s_memrealtime();
+        atomicMax(&stats[26], ~t_start); /* earliest start, complemented */
+        atomicMax(&stats[27], t_end);    /* latest end */
+        atomicAdd(&stats[28], t_end - t_start);
+        atomicAdd(&stats[29], 1ull);
 #ifdef PT_PHASE_TIMING
         for (int k = 0; k < 7; k++)
             atomicAdd(&stats[8 + k], cnt.ph[k]);
@@ -2110,11 +2379,27 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     }
 }
 
+/* Workgroups per CU for the launch bounds: 5 (5 waves/SIMD, VGPRs capped at
+ * 96; A/B on C3: 4 -> 5 +6.6 %, 3 -> -13 %) when that many workgroups' LDS
+ * fits the CU's 160 KB, else as many as fit -- the frame stack grows with
+ * MAXD (depth 16: 4, depth 64: 2), and a cap whose extra wave cannot be
+ * resident would only spill registers. */
+template <class S, int MAXD>
+__device__ constexpr int min_workgroups()
+{
+    constexpr int lds = PT_WPW * ((MAXD + 1) * (int)sizeof(Frame) + PT_FCAP + 16 * PT_RCAP + 2 * PT_SCAP +
+                                  (int)sizeof(Counters) + (int)sizeof(typename S::Root::Ctx));
+    constexpr int alloc = (lds + 1279) / 1280 * 1280; /* gfx950 LDS allocation unit (measured) */
+    constexpr int n = 160 * 1024 / alloc;
+    return n < 1 ? 1 : n > 5 ? 5 : n;
+}
+
 } // namespace ptd
 
-#ifndef PT_MIN_WAVES
-#define PT_MIN_WAVES 5 /* 5 workgroups of 4 waves per CU (5 waves/SIMD, 5 x 31 KB LDS): caps VGPRs \
-                          at 96; A/B on C3: 4 -> 5 +6.6 %, 3 -> -13 % */
+#ifdef PT_MIN_WAVES /* experiment override */
+#define PT_MIN_WG(SCENE, MAXD) PT_MIN_WAVES
+#else
+#define PT_MIN_WG(SCENE, MAXD) (ptd::min_workgroups<SCENE, MAXD>())
 #endif
 
 #define PT_RENDER_ARGS                                                                                     \
@@ -2122,11 +2407,11 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         float *__restrict__ out, const int *__restrict__ pixels, u64 *__restrict__ stats, ptd::PtLaunch lp
 
 #define PT_DEFINE_KERNELS(SCENE, MAXD)                                                                      \
-    extern "C" __global__ __launch_bounds__(64 * PT_WPW, PT_MIN_WAVES) void pt_render_fast(PT_RENDER_ARGS)  \
+    extern "C" __global__ __launch_bounds__(64 * PT_WPW, PT_MIN_WG(SCENE, MAXD)) void pt_render_fast(PT_RENDER_ARGS) \
     {                                                                                                       \
         ptd::render_chunk<SCENE, MAXD, false>(P, imgs, jump, out, pixels, stats, lp);                      \
     }                                                                                                       \
-    extern "C" __global__ __launch_bounds__(64 * PT_WPW, PT_MIN_WAVES) void pt_render_strict(PT_RENDER_ARGS)\
+    extern "C" __global__ __launch_bounds__(64 * PT_WPW, PT_MIN_WG(SCENE, MAXD)) void pt_render_strict(PT_RENDER_ARGS) \
     {                                                                                                       \
         ptd::render_chunk<SCENE, MAXD, true>(P, imgs, jump, out, pixels, stats, lp);                       \
     }

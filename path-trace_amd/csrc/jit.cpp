@@ -84,16 +84,30 @@ const char *kOptions[] = {
     "-fno-slp-vectorize", /* packing pairs of f32 ops into v_pk_* costs more v_mov than it saves (A/B on C3) */
 };
 
-/* experiment hook: extra compiler options, e.g. PT_JIT_OPTIONS="-fno-slp-vectorize" */
+/* experiment hook: extra compiler options, e.g. PT_JIT_OPTIONS="-fno-slp-vectorize".
+ * Options that change floating-point semantics would silently break the
+ * bit-exact contract and are refused; an active hook is announced on stderr. */
 std::vector<std::string> extra_options()
 {
-    std::vector<std::string> v;
-    if (const char *env = getenv("PT_JIT_OPTIONS")) {
+    static const std::vector<std::string> v = [] {
+        std::vector<std::string> r;
+        const char *env = getenv("PT_JIT_OPTIONS");
+        if (!env || !*env)
+            return r;
+        static const char *banned[] = {"fast-math", "Ofast", "fp-contract", "denormal", "flush", "finite-math",
+                                       "unsafe", "associative", "reciprocal", "signed-zeros", "approx",
+                                       "correctly-rounded", "fp-model", "ffp-"};
         std::istringstream in(env);
         std::string o;
-        while (in >> o)
-            v.push_back(o);
-    }
+        while (in >> o) {
+            for (const char *b : banned)
+                if (o.find(b) != std::string::npos)
+                    throw Error(PT_ERR_ARG, "PT_JIT_OPTIONS: '" + o + "' would change floating-point semantics");
+            r.push_back(o);
+        }
+        fprintf(stderr, "pt: experiment hook PT_JIT_OPTIONS=\"%s\" active\n", env);
+        return r;
+    }();
     return v;
 }
 

@@ -568,9 +568,14 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
          * every resident wave a few chunks takes fewer, so one wave does not
          * trace many samples of one expensive pixel while others idle */
         const long long waves = (long long)ds.resident_blocks * ds.wpw;
-        int chunk = 32;
-        if (const char *env = getenv("PT_CHUNK_MAX")) /* experiment hook (1..64) */
-            chunk = std::max(1, std::min(64, atoi(env)));
+        static const int chunk_max = [] {
+            const char *env = getenv("PT_CHUNK_MAX"); /* experiment hook (1..64) */
+            if (!env || !*env)
+                return 32;
+            fprintf(stderr, "pt: experiment hook PT_CHUNK_MAX=%s active\n", env);
+            return std::max(1, std::min(64, atoi(env)));
+        }();
+        int chunk = chunk_max;
         while (chunk > 1 && n_items / chunk < 4 * waves) chunk /= 2;
         long long chunks = (n_items + chunk - 1) / chunk;
         const int wpw = ds.wpw;
@@ -649,6 +654,9 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
         st->rounds = c[3];
         st->slow_queries = c[6];
         st->dark_queries = c[7];
+        st->mid_queries = c[24];
+        if (c[29])
+            st->wave_ms = (double)c[28] * (double)st->launches / (double)c[29] / 1e5; /* 100 MHz clock */
         if (getenv("PT_PHASE_DUMP")) /* profiling builds (PT_PHASE_TIMING): per-phase wave cycles */
         {
             fprintf(stderr, "pt_phases");

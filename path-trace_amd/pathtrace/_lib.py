@@ -39,7 +39,8 @@ class RenderStats(ctypes.Structure):
                 ("samples", ctypes.c_uint64), ("queries", ctypes.c_uint64), ("leaf_queries", ctypes.c_uint64),
                 ("attempts", ctypes.c_uint64), ("rounds", ctypes.c_uint64), ("sphere_tests", ctypes.c_uint64),
                 ("sphere_hits", ctypes.c_uint64), ("plane_tests", ctypes.c_uint64),
-                ("slow_queries", ctypes.c_uint64), ("dark_queries", ctypes.c_uint64)]
+                ("slow_queries", ctypes.c_uint64), ("dark_queries", ctypes.c_uint64),
+                ("mid_queries", ctypes.c_uint64), ("wave_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -175,3 +175,18 @@ def test_fast_math_paths_bitexact(built):
     from pathtrace import _lib
     bad = _lib.selftest_math(n=1 << 28, seed=12345)
     assert bad == {"sqrt": 0, "div": 0, "normalize": 0}, bad
+
+
+@pytest.mark.parametrize("cap", [3, 40])
+def test_round_cut_paths_bitexact(built, tmp_path, monkeypatch, cap):
+    """A generation round normally takes all 512 of its attempts at once (the
+    whole-round path); the per-half replay handles rounds that stop early.
+    PT_ROOM_CAP caps the free ring slots a round may fill, so nearly every
+    round ends at a ring cut and runs the general replay: the pixels stay
+    bit-identical to the oracle."""
+    monkeypatch.setenv("PT_DEVICE_DEFINES", "PT_ROOM_CAP=%d" % cap)
+    root = scenes.scene_p1()
+    W, H, spp, depth = 40, 24, 6, 8
+    g = pt.render(root, W, H, spp, depth)
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_GROUP64)
+    assert_bits(g, o, "PT_ROOM_CAP=%d" % cap)

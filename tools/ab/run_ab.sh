@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU parity suite on the built-in library, then interleaved C3 A/B probes and
 # a small C2 probe per header.  usage: tools/ab/run_ab.sh OUT headerA headerB
+# (a baseline header: git show REV:path-trace_amd/csrc/device/pt_device.h > /tmp/prev.h)
 OUT=$1; shift
 bash tools/gpu_check.sh "$OUT" || exit $?
 bash tools/ab_probe.sh 16 2 "$@" || exit $?

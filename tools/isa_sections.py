@@ -27,7 +27,7 @@ for line in sect.splitlines():
     if not parts or parts[0].endswith(">:"):
         continue
     m = re.match(r"s_nop (\d+)", line.strip())
-    if parts[0] == "s_nop" and len(parts) > 1 and parts[1] in ("8", "9", "10", "11", "12", "13", "14", "15"):
+    if parts[0] == "s_nop" and len(parts) > 1 and parts[1] in ("8", "9", "10", "11", "12", "13", "14", "15", "16", "17"):
         cur = int(parts[1])
         counts[cur]["__markers"] += 1
         continue

@@ -18,4 +18,6 @@ dt = time.time() - t
 ms = st["kernel_ms"]
 print(json.dumps({"spp": spp, "order": order, "wall_s": dt, "kernel_ms": ms,
                   "Msamples_per_s": 1920 * 1080 * spp / ms / 1e3,
-                  "queries_per_sample": st["queries"] / st["samples"], **st}))
+                  "queries_per_sample": st["queries"] / st["samples"],
+                  "Msamples_per_s_waves": 1920 * 1080 * spp / st["wave_ms"] / 1e3 if st.get("wave_ms") else None,
+                  **st}))

@@ -13,7 +13,7 @@ env = dict(os.environ, PT_DEVICE_DEFINES=defs, PT_PHASE_DUMP="1")
 r = subprocess.run([sys.executable, os.path.join(here, "perf_probe.py"), spp], env=env, capture_output=True,
                    text=True, timeout=900)
 print(r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "no stdout", r.stderr[-1500:] if r.returncode else "")
-names = ["generation", "stageA", "fastpass", "slowpass", "groupsum", "burst", "sample"]
+names = ["generation", "gen-attempts", "fastpass", "slowpass", "groupsum", "burst", "sample"]
 for line in r.stderr.splitlines():
     if line.startswith("pt_phases"):
         v = [int(x) for x in line.split()[1:]]

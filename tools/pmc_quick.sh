@@ -1,0 +1,16 @@
+#!/bin/bash
+# Two PMC passes (issue mix) of the C3 probe.  usage: tools/pmc_quick.sh OUTDIR [SPP]
+OUT=${1:-gpurun_out/pmcq}; SPP=${2:-64}
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$OUT"; OUT=$(cd "$OUT" && pwd)
+cd /tmp && export TMPDIR=/tmp
+i=0
+run() {
+    i=$((i + 1))
+    timeout -k 10 300 rocprofv3 --pmc "$@" -d "$OUT/p$i" -o p$i --output-format csv -- python3 "$ROOT/tools/perf_probe.py" "$SPP" > "$OUT/p$i.log" 2>&1
+    rc=$?; echo "pass $i: rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+}
+run SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE
+run SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH
+python3 "$ROOT/tools/sum_pmc.py" pt_render_fast "$OUT/p1" "$OUT/p2"
