@@ -324,6 +324,13 @@ __device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin
 __device__ __forceinline__ V3 univ(V3 v) { return mk(unif(v.x), unif(v.y), unif(v.z)); }
 /* all-ones if the wave-uniform p holds, else 0, by scalar arithmetic */
 __device__ __forceinline__ u64 uni_mask(bool p) { return 0ull - (u64)(u32)uni(p ? 1 : 0); }
+/* this lane's bit of the uniform mask m as 0 / 1: one v_cndmask on the mask */
+__device__ __forceinline__ int lane_bit(u64 m)
+{
+    int r;
+    asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(r) : "s"(m));
+    return r;
+}
 /* base + set bits of the uniform mask m in the lanes below this one (v_mbcnt) */
 __device__ __forceinline__ int mbcnt(u64 m, int base)
 {
@@ -1419,6 +1426,7 @@ struct Attempt
     V3 wn;        /* accepted direction (unnormalised in deferred mode)      */
     float factor; /* 1 - (1 - dot(wn, n)) * sc (0 in deferred mode)         */
     u64 A, F, NL; /* wave ballots: accepted, hemisphere-failed, non-leaf    */
+    bool acc;     /* this lane's attempt is accepted (its bit of A)         */
 };
 
 /* The predicates are balloted where they are produced, so they never pass
@@ -1458,6 +1466,7 @@ __device__ __forceinline__ Attempt attempt(u64 s0, V3 n, V3 kR, float sc, float 
     const u64 BB = __ballot(ball), HB = __ballot(hemi);
     a.A = BB & HB;
     a.F = BB & ~HB;
+    a.acc = ball && hemi;
     a.wn = w;
     a.factor = 0.0f;
     a.NL = 0ull;
@@ -1607,137 +1616,144 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
         if (reason < 0 && room) {
             PT_T0(tg);
             PT_MARK(13);
-            /* ---- generation round: lane l evaluates attempts l, 64 + l, ... */
-            Attempt at[PT_KATT];
-            u64 Am[PT_KATT], Fm[PT_KATT], NLm[PT_KATT], Dm[PT_KATT];
+            /* ---- generation round: lane l evaluates attempts l, 64 + l, ...
+             * Each attempt's flag and ring entry are written at once, as if
+             * the whole round were consumed: a round that stops early consumes
+             * a prefix of the accepted attempts, whose writes are the same, and
+             * the rest lie past npos / nkeep, where nothing reads them before
+             * a later round rewrites them.  Kept entries beyond the free ring
+             * slots are not written (they could overwrite pending ones), and a
+             * round consumes no kept child without a slot.  So the masks die
+             * right after their writes, and only the rare round that stops
+             * early needs them again: it evaluates the attempts a second time. */
+            int rem = N - (i + npos);
+            int free_slots = PT_RCAP - (nkeep - keep_sum);
+#ifdef PT_ROOM_CAP
+            free_slots = min(free_slots, PT_ROOM_CAP); /* test hook: force early round ends */
+#endif
+            int ta = 0, tk = 0; /* accepted / kept attempts of the round */
+            u64 nlor = 0ull, Alast = 0ull, Flast = 0ull;
             {
                 u64 sk = A3l * rng.st + ginc;
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k++) {
                     if (k)
                         sk = A64 * sk + g64inc;
-                    at[k] = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
-                    Am[k] = at[k].A;
-                    Fm[k] = at[k].F;
-                    NLm[k] = at[k].NL;
-                    Dm[k] = 0ull;
+                    const Attempt at = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
+                    u64 D = 0ull;
                     if (RAW)
-                        Dm[k] = S::Root::template dark_mask<Emissive<S>>(c0, at[k].wn, e) & raw_mask;
+                        D = S::Root::template dark_mask<Emissive<S>>(c0, at.wn, e) & raw_mask;
+                    const u64 kp = at.A & ~D;
+                    if (at.acc) {
+                        const int kl = lane_bit(kp);
+                        flags[mbcnt(at.A, npos + ta) & (PT_FCAP - 1)] = (unsigned char)kl;
+                        const int ko = mbcnt(kp, tk);
+                        if (kl && ko < free_slots)
+                            ring[(nkeep + ko) & (PT_RCAP - 1)] = make_float4(at.wn.x, at.wn.y, at.wn.z, at.factor);
+                    }
+                    ta += __popcll(at.A);
+                    tk += __popcll(kp);
+                    nlor |= at.NL;
+                    if (k == PT_KATT - 1)
+                        Alast = at.A, Flast = at.F;
                 }
             }
             PT_ACC(cnt, 1, tg); /* the attempts alone (slot 1) */
             cadd(cnt.rounds, 1u);
-            /* ---- replay the sequential consumption rule on the masks */
-            int rem = N - (i + npos);
-            int free_slots = PT_RCAP - (nkeep - keep_sum);
-#ifdef PT_ROOM_CAP
-            free_slots = min(free_slots, PT_ROOM_CAP); /* test hook: force early round ends */
-#endif
-            u64 take[PT_KATT], keep[PT_KATT];
-            int m = 0; /* attempts consumed this round, 1..64*PT_KATT */
-            bool cut = false;
+            if (DEFERRED && KR0)
+                PT_MARK(14); /* the diffuse (scatter coefficient 1) variant */
+            int m; /* attempts consumed this round, 1..64*PT_KATT */
+            int np, nk; /* children / kept children consumed */
             /* Common case: the whole round is consumed -- fewer accepted
              * children than remain, no non-leaf child, a slot for every kept
              * child, and no abort possible (fails <= 487 and at most 512
              * failures this round) -- so every half takes all its accepted
              * attempts, and the consecutive-failure count afterwards is that
              * of the last half, which has an accepted attempt. */
-            int pa[PT_KATT], pk[PT_KATT];
-            int ta = 0, tk = 0;
-            u64 nlor = 0ull;
+            if (nlor == 0ull && ta < rem && tk <= free_slots && fails <= 487 && Alast != 0ull) {
+                const int last = 63 - __builtin_clzll(Alast);
+                fails = (last == 63) ? 0 : __popcll(Flast >> (last + 1));
+                m = 64 * PT_KATT;
+                np = ta;
+                nk = tk;
+            } else {
+                PT_COLD();
+                /* ---- replay the sequential consumption rule half by half on
+                 * the recomputed masks */
+                Attempt at[PT_KATT];
+                u64 Dm[PT_KATT];
+                {
+                    u64 sk = A3l * rng.st + ginc;
 #pragma unroll
-            for (int k = 0; k < PT_KATT; k++) {
-                pa[k] = __popcll(Am[k]);
-                pk[k] = __popcll(Am[k] & ~Dm[k]);
-                ta += pa[k];
-                tk += pk[k];
-                nlor |= NLm[k];
-            }
-            const bool whole = nlor == 0ull && ta < rem && tk <= free_slots && fails <= 487 && Am[PT_KATT - 1] != 0ull;
-            if (whole) {
+                    for (int k = 0; k < PT_KATT; k++) {
+                        if (k)
+                            sk = A64 * sk + g64inc;
+                        at[k] = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
+                        Dm[k] = 0ull;
+                        if (RAW)
+                            Dm[k] = S::Root::template dark_mask<Emissive<S>>(c0, at[k].wn, e) & raw_mask;
+                    }
+                }
+                m = 0;
+                np = nk = 0;
+                bool cut = false;
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k++) {
-                    take[k] = Am[k];
-                    keep[k] = Am[k] & ~Dm[k];
-                }
-                const int last = 63 - __builtin_clzll(Am[PT_KATT - 1]);
-                fails = (last == 63) ? 0 : __popcll(Fm[PT_KATT - 1] >> (last + 1));
-                m = 64 * PT_KATT;
-            }
-            if (!whole) {
-#pragma unroll
-            for (int k = 0; k < PT_KATT; k++) {
-                take[k] = 0ull;
-                keep[k] = 0ull;
-                if (reason < 0 && !cut) {
-                    const int fails_in = fails;
-                    const int c = replay(Am[k], Fm[k], NLm[k], rem, fails, reason, take[k]);
-                    m = 64 * k + c + 1;
-                    rem -= __popcll(Am[k]);
-                    u64 kp = take[k] & ~Dm[k];
-                    if (__popcll(kp) > free_slots) {
-                        /* the slot ring is full: the round ends just before the
-                         * first kept child without a slot (it is drawn again by
-                         * the next round); no stop rule fired before it */
-                        const int pos = nth_set_bit(kp, free_slots + 1);
-                        const u64 pre = (1ull << pos) - 1ull;
-                        take[k] &= pre;
-                        kp &= pre;
-                        const u64 ca = Am[k] & pre;
-                        if (ca) {
-                            const int last = 63 - __builtin_clzll(ca);
-                            fails = __popcll(Fm[k] & pre & ~((2ull << last) - 1ull));
-                        } else {
-                            fails = fails_in + __popcll(Fm[k] & pre);
+                    if (reason < 0 && !cut) {
+                        u64 take = 0ull;
+                        const int fails_in = fails;
+                        const int c = replay(at[k].A, at[k].F, at[k].NL, rem, fails, reason, take);
+                        m = 64 * k + c + 1;
+                        rem -= __popcll(at[k].A);
+                        u64 kp = take & ~Dm[k];
+                        if (__popcll(kp) > free_slots) {
+                            /* the slot ring is full: the round ends just before the
+                             * first kept child without a slot (it is drawn again by
+                             * the next round); no stop rule fired before it */
+                            const int pos = nth_set_bit(kp, free_slots + 1);
+                            const u64 pre = (1ull << pos) - 1ull;
+                            take &= pre;
+                            kp &= pre;
+                            const u64 ca = at[k].A & pre;
+                            if (ca) {
+                                const int last = 63 - __builtin_clzll(ca);
+                                fails = __popcll(at[k].F & pre & ~((2ull << last) - 1ull));
+                            } else {
+                                fails = fails_in + __popcll(at[k].F & pre);
+                            }
+                            reason = -1;
+                            m = 64 * k + pos;
+                            cut = true;
                         }
-                        reason = -1;
-                        m = 64 * k + pos;
-                        cut = true;
+                        free_slots -= __popcll(kp);
+                        np += __popcll(take);
+                        nk += __popcll(kp);
                     }
-                    keep[k] = kp;
-                    free_slots -= __popcll(kp);
                 }
-                pa[k] = __popcll(take[k]);
-                pk[k] = __popcll(keep[k]);
-            }
-            }
-            if (!DEFERRED && reason == B_NONLEAF) {
-                const int l = (m - 1) & 63, kk = (m - 1) >> 6;
-                V3 wn = at[0].wn;
-                float fac = at[0].factor;
+                if (!DEFERRED && reason == B_NONLEAF) {
+                    const int l = (m - 1) & 63, kk = (m - 1) >> 6;
+                    V3 wn = at[0].wn;
+                    float fac = at[0].factor;
 #pragma unroll
-                for (int k = 1; k < PT_KATT; k++)
-                    if (kk == k)
-                        wn = at[k].wn, fac = at[k].factor;
-                const V3 nd = mk(rdlane(wn.x, l), rdlane(wn.y, l), rdlane(wn.z, l));
-                const float nf = rdlane(fac, l);
-                /* w = addFactor / N * factor * reflect; strength = strength / N * addFactor * factor * |reflect| */
-                f.w = (aN * nf) * rc;
-                child.o = hit;
-                child.d = nd;
-                child.strength = (sNa * nf) * abs_rc;
-                child.depth = depth - 1;
+                    for (int k = 1; k < PT_KATT; k++)
+                        if (kk == k)
+                            wn = at[k].wn, fac = at[k].factor;
+                    const V3 nd = mk(rdlane(wn.x, l), rdlane(wn.y, l), rdlane(wn.z, l));
+                    const float nf = rdlane(fac, l);
+                    /* w = addFactor / N * factor * reflect; strength = strength / N * addFactor * factor * |reflect| */
+                    f.w = (aN * nf) * rc;
+                    child.o = hit;
+                    child.d = nd;
+                    child.strength = (sNa * nf) * abs_rc;
+                    child.depth = depth - 1;
+                }
             }
             cadd(cnt.attempts, (u32)m);
-            /* ---- position flags for every consumed child, ring slots for the kept */
-            int p = npos, kb = nkeep;
-#pragma unroll
-            for (int k = 0; k < PT_KATT; k++) {
-                if (lane_in(take[k])) {
-                    const bool kl = lane_in(keep[k]);
-                    flags[mbcnt(take[k], p) & (PT_FCAP - 1)] = kl ? 1 : 0;
-                    if (kl)
-                        ring[mbcnt(keep[k], kb) & (PT_RCAP - 1)] =
-                            make_float4(at[k].wn.x, at[k].wn.y, at[k].wn.z, at[k].factor);
-                }
-                p += pa[k];
-                kb += pk[k];
-            }
-            cadd(cnt.leaf, (u32)(p - npos));
-            cadd(cnt.dark, (u32)((p - npos) - (kb - nkeep)));
-            f_n += kb - nkeep;
-            npos = p;
-            nkeep = kb;
+            cadd(cnt.leaf, (u32)np);
+            cadd(cnt.dark, (u32)(np - nk));
+            f_n += nk;
+            npos += np;
+            nkeep += nk;
             /* ---- advance the sample's stream past the consumed attempts */
             if (m == 64 * PT_KATT)
                 rng.st = Afull * rng.st + gfullinc;
