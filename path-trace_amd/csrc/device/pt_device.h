@@ -378,6 +378,37 @@ __device__ __forceinline__ float wave_tree_sum(float v)
     return rdlane(v, 63);
 }
 
+/* wave_tree_sum of three values at once, the channels interleaved level by
+ * level in one block so that each DPP read of a channel is two instructions
+ * after that channel's previous write (the VALU -> DPP hazard) without nops.
+ * The row-broadcast levels add in place under a row mask (rows 1 and 3, then
+ * row 3): the masked rows keep their value, as the -0.0 padding of
+ * dpp_bcast_add does.  Same tree, same bits as wave_tree_sum (checked by the
+ * GPU parity tests against the oracle's group-64 order).  Needs all 64 lanes
+ * active. */
+__device__ __forceinline__ V3 wave_tree_sum3(V3 v)
+{
+    float x = v.x, y = v.y, z = v.z;
+    u32 sx, sy, sz;
+#define PT_DPP3(CTL) "v_add_f32_dpp %0, %0, %0 " CTL "\n\t"                       \
+                     "v_add_f32_dpp %1, %1, %1 " CTL "\n\t"                       \
+                     "v_add_f32_dpp %2, %2, %2 " CTL "\n\t"
+    asm volatile("s_nop 1\n\t"
+                 PT_DPP3("quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+                 PT_DPP3("quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf")
+                 PT_DPP3("row_half_mirror row_mask:0xf bank_mask:0xf")
+                 PT_DPP3("row_mirror row_mask:0xf bank_mask:0xf")
+                 PT_DPP3("row_bcast:15 row_mask:0xa bank_mask:0xf")
+                 PT_DPP3("row_bcast:31 row_mask:0x8 bank_mask:0xf")
+                 "s_nop 1\n\t"
+                 "v_readlane_b32 %3, %0, 63\n\t"
+                 "v_readlane_b32 %4, %1, 63\n\t"
+                 "v_readlane_b32 %5, %2, 63"
+                 : "+v"(x), "+v"(y), "+v"(z), "=s"(sx), "=s"(sy), "=s"(sz));
+#undef PT_DPP3
+    return mk(__uint_as_float(sx), __uint_as_float(sy), __uint_as_float(sz));
+}
+
 /* ----------------------------------------------------------- CSG spans --- */
 /* Compact span: a boundary is (t, ref); the reference's normal and material
  * (include/span.h:12-120) are functions of ref and recomputed only for the
@@ -1952,7 +1983,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             const int ngrp = final ? (npos + 63) >> 6 : npos >> 6;
             while (gsum < ngrp) {
                 const int cg = min(64, npos - 64 * gsum);
-                const u64 gm = __ballot(lane < cg && flags[(64 * gsum + lane) & (PT_FCAP - 1)]);
+                const bool kl = lane < cg && flags[(64 * gsum + lane) & (PT_FCAP - 1)];
+                const u64 gm = __ballot(kl);
                 const int gk = __popcll(gm);
                 if (keep_sum + gk > resolved)
                     break;
@@ -1960,29 +1992,30 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 V3 term = mk(-0.0f, -0.0f, -0.0f);
                 if (lane < cg)
                     term = Z;
-                if ((gm >> lane) & 1ull) {
-                    const float4 tv = ring[(keep_sum + __popcll(gm & below)) & (PT_RCAP - 1)];
+                if (kl) {
+                    const float4 tv = ring[mbcnt(gm, keep_sum) & (PT_RCAP - 1)];
                     term = mk(tv.x, tv.y, tv.z);
                 }
                 if (!STRICT && gsum + 1 < ngrp) {
                     /* groups finish in batches (a slow pass resolves many at
-                     * once): when the next group is finished too, its three
-                     * tree sums run interleaved with these; retval still adds
-                     * the group sums one after the other */
+                     * once): when the next group is finished too, its tree
+                     * sums run right after these; retval still adds the group
+                     * sums one after the other */
                     const int cg2 = min(64, npos - 64 * (gsum + 1));
-                    const u64 gm2 = __ballot(lane < cg2 && flags[(64 * (gsum + 1) + lane) & (PT_FCAP - 1)]);
+                    const bool kl2 = lane < cg2 && flags[(64 * (gsum + 1) + lane) & (PT_FCAP - 1)];
+                    const u64 gm2 = __ballot(kl2);
                     const int gk2 = __popcll(gm2);
                     if (keep_sum + gk + gk2 <= resolved) {
                         PT_CNT(cnt, 5, 1);
                         V3 term2 = mk(-0.0f, -0.0f, -0.0f);
                         if (lane < cg2)
                             term2 = Z;
-                        if ((gm2 >> lane) & 1ull) {
-                            const float4 tv = ring[(keep_sum + gk + __popcll(gm2 & below)) & (PT_RCAP - 1)];
+                        if (kl2) {
+                            const float4 tv = ring[mbcnt(gm2, keep_sum + gk) & (PT_RCAP - 1)];
                             term2 = mk(tv.x, tv.y, tv.z);
                         }
-                        const V3 g1 = mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
-                        const V3 g2 = mk(wave_tree_sum(term2.x), wave_tree_sum(term2.y), wave_tree_sum(term2.z));
+                        const V3 g1 = wave_tree_sum3(term);
+                        const V3 g2 = wave_tree_sum3(term2);
                         retval = univ(retval + g1);
                         retval = univ(retval + g2);
                         keep_sum += gk + gk2;
@@ -1994,8 +2027,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     for (int j = 0; j < cg; j++)
                         retval = retval + mk(rdlane(term.x, j), rdlane(term.y, j), rdlane(term.z, j));
                 } else {
-                    retval = retval + mk(wave_tree_sum(term.x), wave_tree_sum(term.y), wave_tree_sum(term.z));
-                    retval = univ(retval);
+                    retval = univ(retval + wave_tree_sum3(term));
                 }
                 keep_sum += gk;
                 gsum++;
