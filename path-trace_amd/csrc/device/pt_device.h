@@ -1447,6 +1447,7 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #define PT_FCAP 2048 /* child-position flags per wave (32 groups of 64)               */
 #define PT_SCAP 128  /* mid / slow queue entries (< 128 pending by construction; byte ring numbers) */
 static_assert(64 * PT_KATT <= PT_FCAP / 2, "position flags too few for PT_KATT");
+static_assert(PT_KATT % 2 == 0, "deferred rounds evaluate attempts in pairs");
 #define PT_JUMP_ENTRIES 1025 /* host table: m = 0..1024 attempts */
 static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
 
@@ -1508,6 +1509,45 @@ __device__ __forceinline__ Attempt attempt(u64 s0, V3 n, V3 kR, float sc, float 
         a.NL = __ballot(ball && hemi && !(child_leaf_depth || cs < EPS));
     }
     return a;
+}
+
+/* Two attempts of a deferred burst (attempts k and k + 1 of a lane: engine
+ * states s0a, s0b) in packed f32 (v_pk_fma / v_pk_mul / v_pk_add, one
+ * instruction for both): element-wise the same IEEE operations in the same
+ * order as attempt<true, KR0>, so the same bits. */
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct Attempt2
+{
+    f2 x, y, z;   /* w of the two attempts (unnormalised)  */
+    u64 A[2], F[2];
+    bool acc[2];
+};
+template <bool KR0>
+__device__ __forceinline__ Attempt2 attempt2(u64 s0a, u64 s0b, V3 n, V3 kR)
+{
+    const W2 a1 = lcg_step({(u32)s0a, (u32)(s0a >> 32)}), a2 = lcg_step(a1), a3 = lcg_step(a2);
+    const W2 b1 = lcg_step({(u32)s0b, (u32)(s0b >> 32)}), b2 = lcg_step(b1), b3 = lcg_step(b2);
+    const f2 S = 0x1p-31f, M1 = -1.0f;
+    /* u11: (float)o * 2^-31 - 1, the product exact (see u11) */
+    f2 x = {(float)a1.hi, (float)b1.hi}, y = {(float)a2.hi, (float)b2.hi}, z = {(float)a3.hi, (float)b3.hi};
+    x = __builtin_elementwise_fma(x, S, M1);
+    y = __builtin_elementwise_fma(y, S, M1);
+    z = __builtin_elementwise_fma(z, S, M1);
+    const f2 vv = (x * x + y * y) + z * z; /* dot(v, v) */
+    if (!KR0) {
+        x = x + kR.x;
+        y = y + kR.y;
+        z = z + kR.z;
+    }
+    const f2 nw = (x * n.x + y * n.y) + z * n.z; /* dot(n, w): n.x * w.x == w.x * n.x */
+    Attempt2 r;
+    r.x = x, r.y = y, r.z = z;
+    const bool ba = !(vv.x > 0x1.000002p+0f), bb = !(vv.y > 0x1.000002p+0f);
+    const bool ha = !(nw.x <= EPS), hb = !(nw.y <= EPS);
+    const u64 BA = __ballot(ba), HA = __ballot(ha), BBm = __ballot(bb), HBm = __ballot(hb);
+    r.A[0] = BA & HA, r.F[0] = BA & ~HA, r.acc[0] = ba && ha;
+    r.A[1] = BBm & HBm, r.F[1] = BBm & ~HBm, r.acc[1] = bb && hb;
+    return r;
 }
 
 /* Replays the reference's sequential consumption of one half-round of 64
@@ -1664,26 +1704,47 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 #endif
             int ta = 0, tk = 0; /* accepted / kept attempts of the round */
             u64 nlor = 0ull, Alast = 0ull, Flast = 0ull;
-            {
+            /* one attempt's flag and (kept, with a free slot) ring entry */
+            auto write_attempt = [&](bool acc, u64 A, u64 kp, V3 wn, float factor) {
+                if (acc) {
+                    const int kl = lane_bit(kp);
+                    flags[mbcnt(A, npos + ta) & (PT_FCAP - 1)] = (unsigned char)kl;
+                    const int ko = mbcnt(kp, tk);
+                    if (kl && ko < free_slots)
+                        ring[(nkeep + ko) & (PT_RCAP - 1)] = make_float4(wn.x, wn.y, wn.z, factor);
+                }
+                ta += __popcll(A);
+                tk += __popcll(kp);
+            };
+            if (DEFERRED) {
+                /* pairs of attempts in packed f32 */
+                u64 sk = A3l * rng.st + ginc;
+#pragma unroll
+                for (int k = 0; k < PT_KATT; k += 2) {
+                    if (k)
+                        sk = A64 * sk + g64inc;
+                    const u64 sk1 = A64 * sk + g64inc;
+                    const Attempt2 ap = attempt2<KR0>(sk, sk1, n, kR);
+                    sk = sk1;
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
+                        u64 D = 0ull;
+                        if (RAW)
+                            D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
+                        write_attempt(ap.acc[h], ap.A[h], ap.A[h] & ~D, wn, 0.0f);
+                        if (k + h == PT_KATT - 1)
+                            Alast = ap.A[h], Flast = ap.F[h];
+                    }
+                }
+            } else {
                 u64 sk = A3l * rng.st + ginc;
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k++) {
                     if (k)
                         sk = A64 * sk + g64inc;
                     const Attempt at = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
-                    u64 D = 0ull;
-                    if (RAW)
-                        D = S::Root::template dark_mask<Emissive<S>>(c0, at.wn, e) & raw_mask;
-                    const u64 kp = at.A & ~D;
-                    if (at.acc) {
-                        const int kl = lane_bit(kp);
-                        flags[mbcnt(at.A, npos + ta) & (PT_FCAP - 1)] = (unsigned char)kl;
-                        const int ko = mbcnt(kp, tk);
-                        if (kl && ko < free_slots)
-                            ring[(nkeep + ko) & (PT_RCAP - 1)] = make_float4(at.wn.x, at.wn.y, at.wn.z, at.factor);
-                    }
-                    ta += __popcll(at.A);
-                    tk += __popcll(kp);
+                    write_attempt(at.acc, at.A, at.A, at.wn, at.factor);
                     nlor |= at.NL;
                     if (k == PT_KATT - 1)
                         Alast = at.A, Flast = at.F;
