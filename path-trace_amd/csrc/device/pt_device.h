@@ -378,7 +378,8 @@ __device__ __forceinline__ float wave_tree_sum(float v)
     return rdlane(v, 63);
 }
 
-/* wave_tree_sum of three values at once, the channels interleaved level by
+/* acc + wave_tree_sum(v), channel by channel (acc wave-uniform, added as
+ * acc + sum: IEEE addition commutes), the three tree sums interleaved level by
  * level in one block so that each DPP read of a channel is two instructions
  * after that channel's previous write (the VALU -> DPP hazard) without nops.
  * The row-broadcast levels add in place under a row mask (rows 1 and 3, then
@@ -386,7 +387,7 @@ __device__ __forceinline__ float wave_tree_sum(float v)
  * dpp_bcast_add does.  Same tree, same bits as wave_tree_sum (checked by the
  * GPU parity tests against the oracle's group-64 order).  Needs all 64 lanes
  * active. */
-__device__ __forceinline__ V3 wave_tree_sum3(V3 v)
+__device__ __forceinline__ V3 wave_tree_sum3_add(V3 v, V3 acc)
 {
     float x = v.x, y = v.y, z = v.z;
     u32 sx, sy, sz;
@@ -400,11 +401,15 @@ __device__ __forceinline__ V3 wave_tree_sum3(V3 v)
                  PT_DPP3("row_mirror row_mask:0xf bank_mask:0xf")
                  PT_DPP3("row_bcast:15 row_mask:0xa bank_mask:0xf")
                  PT_DPP3("row_bcast:31 row_mask:0x8 bank_mask:0xf")
+                 "v_add_f32 %0, %6, %0\n\t"
+                 "v_add_f32 %1, %7, %1\n\t"
+                 "v_add_f32 %2, %8, %2\n\t"
                  "s_nop 1\n\t"
                  "v_readlane_b32 %3, %0, 63\n\t"
                  "v_readlane_b32 %4, %1, 63\n\t"
                  "v_readlane_b32 %5, %2, 63"
-                 : "+v"(x), "+v"(y), "+v"(z), "=s"(sx), "=s"(sy), "=s"(sz));
+                 : "+v"(x), "+v"(y), "+v"(z), "=s"(sx), "=s"(sy), "=s"(sz)
+                 : "s"(acc.x), "s"(acc.y), "s"(acc.z));
 #undef PT_DPP3
     return mk(__uint_as_float(sx), __uint_as_float(sy), __uint_as_float(sz));
 }
@@ -2075,10 +2080,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                             const float4 tv = ring[mbcnt(gm2, keep_sum + gk) & (PT_RCAP - 1)];
                             term2 = mk(tv.x, tv.y, tv.z);
                         }
-                        const V3 g1 = wave_tree_sum3(term);
-                        const V3 g2 = wave_tree_sum3(term2);
-                        retval = univ(retval + g1);
-                        retval = univ(retval + g2);
+                        retval = wave_tree_sum3_add(term, retval);
+                        retval = wave_tree_sum3_add(term2, retval);
                         keep_sum += gk + gk2;
                         gsum += 2;
                         continue;
@@ -2088,7 +2091,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     for (int j = 0; j < cg; j++)
                         retval = retval + mk(rdlane(term.x, j), rdlane(term.y, j), rdlane(term.z, j));
                 } else {
-                    retval = univ(retval + wave_tree_sum3(term));
+                    retval = wave_tree_sum3_add(term, retval);
                 }
                 keep_sum += gk;
                 gsum++;
