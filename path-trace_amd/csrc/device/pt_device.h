@@ -1544,7 +1544,22 @@ __device__ __forceinline__ Attempt2 attempt2(u64 s0a, u64 s0b, V3 n, V3 kR)
         y = y + kR.y;
         z = z + kR.z;
     }
+#ifndef PT_HEMI_MODE
+#define PT_HEMI_MODE 1 /* A/B on C3: 1 +0.8 % over 0, 2 the same as 0 */
+#endif
+#if PT_HEMI_MODE == 1
+    /* dot(n, w) per attempt on scalar n (3 SGPRs rather than 3 splatted pairs) */
+    const f2 nw = {(n.x * x.x + n.y * y.x) + n.z * z.x, (n.x * x.y + n.y * y.y) + n.z * z.y};
+#elif PT_HEMI_MODE == 2
+    /* the splatted normal in VGPRs (the asm hides its uniformity) */
+    float vnx, vny, vnz;
+    asm("v_mov_b32 %0, %1" : "=v"(vnx) : "s"(n.x));
+    asm("v_mov_b32 %0, %1" : "=v"(vny) : "s"(n.y));
+    asm("v_mov_b32 %0, %1" : "=v"(vnz) : "s"(n.z));
+    const f2 nw = (x * vnx + y * vny) + z * vnz;
+#else
     const f2 nw = (x * n.x + y * n.y) + z * n.z; /* dot(n, w): n.x * w.x == w.x * n.x */
+#endif
     Attempt2 r;
     r.x = x, r.y = y, r.z = z;
     const bool ba = !(vv.x > 0x1.000002p+0f), bb = !(vv.y > 0x1.000002p+0f);

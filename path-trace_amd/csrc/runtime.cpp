@@ -664,6 +664,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
                 fprintf(stderr, " %llu", (unsigned long long)c[k]);
             for (int k = 16; k < 24; k++)
                 fprintf(stderr, " %llu", (unsigned long long)c[k]);
+            fprintf(stderr, " %llu", (unsigned long long)c[25]); /* whole chunk loop */
             fprintf(stderr, "\n");
         }
         st->sphere_tests = st->queries * (uint64_t)g.n_spheres;

@@ -21,7 +21,10 @@ for line in r.stderr.splitlines():
         for n, x in zip(names, v):
             print("%-12s %6.1f%%" % (n, 100.0 * x / tot))
         print("%-12s %6.1f%%" % ("spine", 100.0 * (v[6] - v[5]) / tot))
-        print("%-12s %6.1f%%" % ("burst-other", 100.0 * (v[5] - sum(v[:5])) / tot))
+        print("%-12s %6.1f%%" % ("burst-other", 100.0 * (v[5] - v[0] - sum(v[2:5])) / tot))
+        if len(v) >= 16 and v[15]:
+            print("%-12s %6.1f%%  (of the whole chunk loop: lane-parallel camera queries, lane samples, writes)" %
+                  ("sample/loop", 100.0 * tot / v[15]))
         if len(v) >= 15:
             import json as _j
             smp = _j.loads(r.stdout.strip().splitlines()[-1])["samples"]
