@@ -33,19 +33,26 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "path-trace_amd"), os.path.join(ROOT, "oracle")]
 
 VALU_PEAK_TOPS = 78.6  # 256 CU x 128 FP32 lanes/clk x 2.4 GHz, no FMA (contraction off for parity)
-# SURVEY.md s8(d) op model calibrated by tools/calibrate_ops.py C3 8192 32 (oracle event counts)
-OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75}
-# HBM bytes per sample of the render kernel from the PMC passes of this same
-# command (tools/pmc_traffic.sh; FETCH_SIZE + WRITE_SIZE, gfx950-corrected)
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "round1", "traffic_C3.json")
+# SURVEY.md s8(d) op model calibrated by tools/calibrate_ops.py (oracle event
+# counts on hashed pixels): C3 8192 px x 32 spp, C2 512 px x 4 spp
+OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 614.78}
+# Counter evidence of this same command (tools/pmc_bench.sh: rocprofv3 --pmc
+# passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 + WRITE_SIZE)
+PMC_JSON = os.path.join(ROOT, "profiles", "round2", "pmc_bench_%s.json")
+# bounded CPU samples (~10-30 s of reference work on the box's 16 host threads)
+CPU_PIXELS = {"C1": 2048, "C2": 512, "C3": 2048, "C4": 2048, "C5": 64}
+# C5 (3840x2160 x 8192 spp, 68 G samples) is timed on a hashed pixel subset at
+# its full spp and depth: at that size the reference camera (|d| = 4320) hides
+# everything nearer than 4.32 units, so the frame is the sky box and the skybox
+# sphere and per-pixel cost is uniform enough for a subset to represent it
+SUBSET = {"C5": 65536}
 
 
-def traffic_per_launch(samples_per_launch: int):
+def pmc_evidence(cfg_name: str):
     try:
-        with open(TRAFFIC_JSON) as f:
-            t = json.load(f)
-        return round(t["bytes_per_sample"] * samples_per_launch)
-    except (OSError, KeyError, ValueError):
+        with open(PMC_JSON % cfg_name) as f:
+            return json.load(f)
+    except (OSError, ValueError):
         return None
 
 
@@ -56,12 +63,18 @@ def parse():
     ap.add_argument("--warmup", type=int, default=0)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override (for quick local probes only; invalid metric)")
-    ap.add_argument("--cpu-pixels", type=int, default=2048)
+    ap.add_argument("--cpu-pixels", type=int, default=0, help="0 = the config's bounded sample (CPU_PIXELS)")
+    ap.add_argument("--subset", type=int, default=-1,
+                    help="render only this many hashed pixels at full spp (-1 = config default, 0 = whole frame)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS "
                          "when set (the GPU box exports its per-GPU CPU share there)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--order", default="fast")
+    ap.add_argument("--split", choices=["samples", "tiles"], default="samples",
+                    help="N>1: each rank renders every pixel for its share of the samples (balanced to noise), "
+                         "or the hashed 16x16 tiles it owns (bit-identical to 1 GPU, measured 1.19 max/mean "
+                         "shard imbalance on C4)")
     return ap.parse_args()
 
 
@@ -77,7 +90,7 @@ def cpu_threads(requested: int) -> int:
     return max(1, n)
 
 
-def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps):
+def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps, within=None):
     """The reference's own hot path (tracePixel per (pixel, sample), src/test.cpp:450;
     one std::thread per host core as RenderBlock's pool, src/test.cpp:204) over a
     hashed pixel subset of the same frame.  Per-sample cost is bimodal (sky vs
@@ -86,7 +99,10 @@ def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps):
     proportional to span queries)."""
     import oracle_py as O
     rng = np.random.default_rng(0x5EED)
-    pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
+    pool = cfg.width * cfg.height if within is None else np.asarray(within)
+    pix = np.sort(rng.choice(pool, min(npix, len(pool) if within is not None else npix), replace=False))
+    pix = pix.astype(np.int32)
+    npix = len(pix)
     qps = None
     if O.ref_available():
         kind = "reference"
@@ -136,11 +152,20 @@ def main():
     W, H = cfg.width, cfg.height
     root = cfg.scene()
     ds = pt.DeviceScene(root)
-    mine = ptdist.rank_pixels(W, H, rank, world)
+    subset = SUBSET.get(cfg.name, 0) if args.subset < 0 else args.subset
+    by_samples = world > 1 and args.split == "samples"
+    mine = ptdist.rank_pixels(W, H, rank, 1 if by_samples else world)
+    s_begin, s_count = (rank * spp // world, (rank + 1) * spp // world - rank * spp // world) if by_samples \
+        else (0, spp)
+    if subset:
+        rng = np.random.default_rng(0x5EED)
+        keep = np.sort(rng.choice(W * H, subset, replace=False)).astype(np.int32)
+        mine = np.intersect1d(mine, keep).astype(np.int32)
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream()
-    params, keep = pt.make_params(W, H, spp, cfg.depth, screen=cfg.screen, order=args.order, device=local,
-                                  pixels=None if world == 1 else mine, max_buffer_bytes=40 << 30)
+    params, keep = pt.make_params(W, H, s_count, cfg.depth, screen=cfg.screen, order=args.order, device=local,
+                                  pixels=None if ((world == 1 or by_samples) and not subset) else mine,
+                                  max_buffer_bytes=40 << 30, sample_begin=s_begin, sum_only=by_samples)
     # untimed: load the code object, upload the scene, allocate every buffer
     pt.prepare(ds, params)
     torch.cuda.synchronize()
@@ -150,6 +175,8 @@ def main():
         st = pt.render_device(ds, params, fb.data_ptr(), stream.cuda_stream, stats=True)
         if dist is not None:
             dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+            if by_samples and rank == 0:
+                fb.div_(float(spp))  # the ranks' sample sums, summed, over spp: tracePixel's mean
         return st
 
     for _ in range(args.warmup):
@@ -175,7 +202,8 @@ def main():
         queries = int(q[0])
 
     if rank == 0:
-        samples = W * H * spp * args.steps
+        npix_total = subset if subset else W * H
+        samples = npix_total * spp * args.steps
         value = samples / elapsed / 1e6
         frame = fb.view(H, W, 3).cpu().numpy()
         out = {
@@ -183,25 +211,37 @@ def main():
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "%s: %dx%d, %d spp, depth %d, %s" % (cfg.name, W, H, spp, cfg.depth, cfg.note),
-                       "order": args.order, "sharding": "16x16 tiles hashed over ranks + RCCL reduce"},
+            "config": {"workload": "%s: %dx%d, %d spp, depth %d, %s%s" % (
+                cfg.name, W, H, spp, cfg.depth, cfg.note,
+                ("; timed on %d hashed pixels at full spp" % subset) if subset else ""),
+                       "order": args.order,
+                       "sharding": ("every pixel, spp split over ranks, per-pixel sums + RCCL reduce" if by_samples
+                                    else "16x16 tiles hashed over ranks + RCCL reduce")},
+            "samples_per_step": npix_total * spp,
             "queries_per_sample": round(queries / samples, 2),
         }
         opq = OPS_PER_QUERY.get(cfg.name)
         if opq:
             ops_per_launch = opq * queries / (args.steps * launches_per_step * world)
             achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12
-            samples_per_launch = W * H * spp // (launches_per_step * world)
+            ev = pmc_evidence(cfg.name) if (not subset and spp == cfg.spp) else None
             out["roofline"] = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS,
                                "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
-                               "traffic": traffic_per_launch(samples_per_launch) if cfg.name == "C3" else None,
-                               "traffic_unit": "bytes/launch (PMC, %s)" % os.path.relpath(TRAFFIC_JSON, ROOT),
+                               "traffic": round(ev["hbm_bytes_per_launch"]) if ev else None,
                                "kernel": "pt_render_fast", "avg_launch_ms": round(kernel_ms, 2),
                                "ops_per_query": opq}
+            if ev:
+                out["roofline"].update({
+                    "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE, %s)" %
+                                    os.path.relpath(PMC_JSON % cfg.name, ROOT),
+                    "valu_busy": round(ev["valu_busy"], 4), "salu_busy": round(ev["salu_busy"], 4),
+                    "hbm_GBps": round(ev["hbm_GBps"], 2), "hbm_peak_GBps": 8000.0})
         if not args.no_cpu and world == 1:
             try:
-                pix, ref, cb = cpu_baseline(cfg, to_text(root, "/tmp/pt_bench_img"), spp, args.cpu_pixels,
-                                            cpu_threads(args.cpu_threads), queries / samples)
+                npx = args.cpu_pixels or CPU_PIXELS.get(cfg.name, 512)
+                pix, ref, cb = cpu_baseline(cfg, to_text(root, "/tmp/pt_bench_img"), spp, npx,
+                                            cpu_threads(args.cpu_threads), queries / samples,
+                                            mine if subset else None)
                 gpu = frame.reshape(-1, 3)[pix]
                 out["rmse_vs_cpu_ref"] = [float(v) for v in
                                           np.sqrt(np.mean((gpu.astype(np.float64) - ref) ** 2, axis=0))]

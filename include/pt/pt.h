@@ -129,6 +129,11 @@ typedef struct pt_render_params {
     int grid_width;                /* pixel index = y * grid_width + x (0 = width); > width
                                       addresses pixels past the right / bottom edge, as the
                                       adaptive caller's block edges do                          */
+    int sample_begin;              /* engine sample index of this call's first sample: the call
+                                      renders samples sample_begin .. sample_begin + spp - 1 of
+                                      each pixel (a rank's share when samples are split)        */
+    int sum_only;                  /* nonzero: write each pixel's sum of those samples, in
+                                      sample order, without the division by spp               */
 } pt_render_params;
 
 typedef struct pt_render_stats {

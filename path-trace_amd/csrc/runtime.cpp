@@ -481,6 +481,8 @@ void validate(const pt_render_params *p)
         throw Error(PT_ERR_ARG, "frame too large");
     if (p->spp >= (1 << 20))
         throw Error(PT_ERR_ARG, "spp must be < 2^20 (engine key layout)");
+    if (p->sample_begin < 0 || (int64_t)p->sample_begin + p->spp > (1 << 20))
+        throw Error(PT_ERR_ARG, "samples must lie in [0, 2^20) (engine key layout)");
     if (p->depth < 0 || p->depth > 64)
         throw Error(PT_ERR_ARG, "depth must be in [0, 64]");
     if (p->order != PT_ORDER_GROUP64 && p->order != PT_ORDER_REFERENCE)
@@ -591,7 +593,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             lp.sw = p->screen_w, lp.sh = p->screen_h, lp.dist = p->screen_dist;
             lp.depth = p->depth;
             lp.nsamp = nsamp;
-            lp.s0 = s0;
+            lp.s0 = p->sample_begin + s0;
             lp.gw = p->grid_width > 0 ? p->grid_width : p->width;
             lp.chunk = chunk;
             const float *Pp = ds.P.p;
@@ -618,7 +620,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             const int *pp = dpix;
             long long ns = npix;
             int first = s0 == 0, last = s0 + nsamp == p->spp;
-            float spp = (float)p->spp;
+            float spp = p->sum_only ? 1.0f : (float)p->spp; /* x / 1 == x: the raw sum */
             void *args[] = {&in, &acc, &fb, &pp, &ns, &nsamp, &first, &last, &spp};
             unsigned blocks = (unsigned)((npix + 255) / 256);
             int e0 = (int)evs.size();

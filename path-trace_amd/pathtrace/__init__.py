@@ -122,7 +122,7 @@ class DeviceScene:
 
 
 def make_params(width, height, spp, depth, screen=None, seed=0x5EED, order="fast", device=0, pixels=None,
-                max_buffer_bytes=0, grid_width=0):
+                max_buffer_bytes=0, grid_width=0, sample_begin=0, sum_only=False):
     sw, sh, dist = screen if screen is not None else (float(width), float(height), float(2 * min(width, height)))
     p = RenderParams()
     p.width, p.height, p.spp, p.depth = int(width), int(height), int(spp), int(depth)
@@ -140,15 +140,19 @@ def make_params(width, height, spp, depth, screen=None, seed=0x5EED, order="fast
         p.npixels = 0
     p.max_buffer_bytes = int(max_buffer_bytes)
     p.grid_width = int(grid_width)
+    p.sample_begin = int(sample_begin)
+    p.sum_only = 1 if sum_only else 0
     return p, keep
 
 
 def render(scene, width: int, height: int, spp: int, depth: int, screen=None, seed: int = 0x5EED,
            order="fast", pixels: Optional[Sequence[int]] = None, device: int = 0, stats: bool = False,
-           max_buffer_bytes: int = 0):
-    """tracePixel means for every pixel (H x W x 3), or for `pixels` (n x 3)."""
+           max_buffer_bytes: int = 0, sample_begin: int = 0, sum_only: bool = False):
+    """tracePixel means for every pixel (H x W x 3), or for `pixels` (n x 3);
+    with sum_only, the per-pixel sums of samples sample_begin .. + spp - 1."""
     ds = scene if isinstance(scene, DeviceScene) else DeviceScene(scene)
-    p, keep = make_params(width, height, spp, depth, screen, seed, order, device, pixels, max_buffer_bytes)
+    p, keep = make_params(width, height, spp, depth, screen, seed, order, device, pixels, max_buffer_bytes,
+                          sample_begin=sample_begin, sum_only=sum_only)
     n = (len(keep) if keep is not None else width * height)
     out = np.zeros((n, 3), dtype=np.float32)
     st = RenderStats()

@@ -26,7 +26,8 @@ class RenderParams(ctypes.Structure):
                 ("screen_w", ctypes.c_float), ("screen_h", ctypes.c_float), ("screen_dist", ctypes.c_float),
                 ("seed", ctypes.c_uint64), ("order", ctypes.c_int), ("device", ctypes.c_int),
                 ("pixels", ctypes.POINTER(ctypes.c_int32)), ("npixels", ctypes.c_int64),
-                ("max_buffer_bytes", ctypes.c_int64), ("grid_width", ctypes.c_int)]
+                ("max_buffer_bytes", ctypes.c_int64), ("grid_width", ctypes.c_int),
+                ("sample_begin", ctypes.c_int), ("sum_only", ctypes.c_int)]
 
 
 class AdaptiveParams(ctypes.Structure):

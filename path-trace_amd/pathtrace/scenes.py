@@ -13,6 +13,7 @@ screen_h = H, screen_dist = 2 * min(W, H), origin 0, looking down -z.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Callable, Dict
 
@@ -55,6 +56,22 @@ def scene_p1():
     return Union(left, Union(right, Plane((0, 0, 1), 200, m["sky"])))
 
 
+# The reference's own input images, shipped as data:
+# test2.hdr (640x480) stands in for the missing stpeters_probe.hdr (C2),
+# test.hdr (1280x1509) for the missing Serpentine_Valley_3k.hdr (C5), and
+# sky01/*.png (6 x 877^2) is the skybox of makeSkyBox (src/test.cpp:88-95).
+ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "assets")
+_images: Dict[str, Image] = {}
+
+
+def asset_image(name: str) -> Image:
+    """Image(fileName) of a reference asset, loaded once per process by the
+    product's own loaders (pt_image_load_hdr / pt_image_load_png)."""
+    if name not in _images:
+        _images[name] = Image(path=os.path.join(ASSETS, name))
+    return _images[name]
+
+
 def procedural_env(w: int, h: int, seed: int = 7) -> Image:
     """Deterministic synthetic HDR environment map (substitute for the missing
     stpeters_probe.hdr / Serpentine_Valley_3k.hdr): a sky
@@ -86,12 +103,13 @@ def procedural_face(size: int, face: int) -> Image:
     return Image(img)
 
 
-def scene_c2(env_w: int = 640, env_h: int = 480):
+def scene_c2(procedural: bool = False):
     """C2: eight spheres of the demo material mix over a ground plane inside six
     inward sky half-spaces at distance 200 carrying a mirror-ball sky map
-    (reference makeSkyMirrorSphere, src/test.cpp:97-100 and :134-140)."""
+    (reference makeSkyMirrorSphere, src/test.cpp:97-100 and :134-140) of
+    test2.hdr (procedural=True: a synthetic 640x480 map, for CPU-only tests)."""
     m = materials()
-    env = procedural_env(env_w, env_h)
+    env = procedural_env(640, 480) if procedural else asset_image("test2.hdr")
     sky = Material(ColorTexture(0), ColorTexture(0),
                    MultiplyTexture((1, 1, 1), MirrorBallSkymapTexture(ImageTexture(env))))
     # the demo's material mix (src/test.cpp:109-118) minus matBrightDiffuseWhite:
@@ -109,20 +127,24 @@ def scene_c2(env_w: int = 640, env_h: int = 480):
     return union_array(objs)
 
 
-def scene_c5(env_w: int = 1024, env_h: int = 512, face: int = 128):
-    """C5: the reference demo world (src/test.cpp:107-145) with a procedural
-    env map in place of Serpentine_Valley_3k.hdr (kept under rotateX(pi/2) and
-    scale 0.01) plus a sphere whose emissive is an ImageSkyboxTexture
-    (makeSkyBox, src/test.cpp:88-95) with procedural faces for sky01/*.png."""
+def scene_c5(procedural: bool = False):
+    """C5: the reference demo world (src/test.cpp:107-145) with test.hdr in
+    place of Serpentine_Valley_3k.hdr (kept under rotateX(pi/2) and scale 0.01)
+    plus a sphere whose emissive is an ImageSkyboxTexture of sky01/*.png
+    (makeSkyBox, src/test.cpp:88-95).  procedural=True swaps in small
+    synthetic images (CPU-only tests)."""
     m = materials()
-    env = procedural_env(env_w, env_h, seed=11)
+    env = procedural_env(1024, 512, seed=11) if procedural else asset_image("test.hdr")
     sky_sph = Material(ColorTexture(0), ColorTexture(0),
                        MultiplyTexture((0.01, 0.01, 0.01), SphericalCoordinatesSkymapTexture(ImageTexture(env))))
     sky = transform_material(Matrix.rotateX(2 * math.pi / 4), sky_sph)
     diffuse, glass, emitW = m["diffuse"], m["glass"], m["emitW"]
     dw = transform_material(Matrix.translate(-1, 0, 4), diffuse)
     ew = transform_material(Matrix.translate(-1, 0, 4), emitW)
-    faces = [procedural_face(face, k) for k in range(6)]
+    if procedural:
+        faces = [procedural_face(128, k) for k in range(6)]
+    else:
+        faces = [asset_image("sky01/%s.png" % f) for f in ("top", "bottom", "left", "right", "front", "back")]
     skybox = Material(ColorTexture(0), ColorTexture(0), ImageSkyboxTexture(*faces))
 
     def make_lens(position, orientation, radius, sphere_radius, material):
@@ -168,8 +190,9 @@ class Config:
 
 CONFIGS: Dict[str, Config] = {
     "C1": Config("C1", 256, 256, 16, 4, scene_p0, note="plumbing; CPU reference path"),
-    "C2": Config("C2", 1280, 720, 256, 16, scene_c2, note="8 spheres + plane + mirror-ball env (procedural)"),
+    "C2": Config("C2", 1280, 720, 256, 16, scene_c2, note="8 spheres + plane + mirror-ball env (test2.hdr)"),
     "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG"),
     "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene, tiles over 8 GPUs + RCCL reduce"),
-    "C5": Config("C5", 3840, 2160, 8192, 16, scene_c5, gpus=8, note="demo world + env map + skybox"),
+    "C5": Config("C5", 3840, 2160, 8192, 16, scene_c5, gpus=8,
+                 note="demo world + test.hdr spherical env + sky01 skybox"),
 }

@@ -63,3 +63,42 @@ def test_gloo_two_ranks_bitexact(built, tmp_path):
     got = np.load(out).reshape(-1, 3)
     want = O.render(txt, W, H, spp, depth, order=O.ORDER_GROUP64)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def _split_worker(rank, world, port, txt, W, H, spp, depth, out_path):
+    import torch
+    import torch.distributed as dist
+    import oracle_py as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, e = rank * spp // world, (rank + 1) * spp // world
+    per = O.render(txt, W, H, spp, depth, threads=2, order=O.ORDER_GROUP64, per_sample=True)[:, b:e]
+    acc = np.zeros((W * H, 3), dtype=np.float32)
+    for s in range(per.shape[1]):  # this rank's samples, summed in sample order (sum_only)
+        acc = (acc + per[:, s]).astype(np.float32)
+    fb = torch.from_numpy(acc.reshape(-1).copy())
+    ptdist.reduce_frame(fb)
+    if rank == 0:
+        fb.div_(float(spp))
+        np.save(out_path, fb.numpy())
+    dist.destroy_process_group()
+
+
+def test_gloo_sample_split_two_ranks(built, tmp_path):
+    """bench.py's default N>1 split: every rank renders all pixels for its
+    share of the samples and sends per-pixel sums; rank 0 divides the reduced
+    sums by spp.  Equals the single-process frame within float rounding of the
+    changed summation order (RMSE far below the 1e-3 bar)."""
+    import torch.multiprocessing as mp
+    import oracle_py as O
+    from pathtrace import scenes
+    from pathtrace.scene import to_text
+    W, H, spp, depth = 24, 16, 6, 8
+    txt = to_text(scenes.scene_p1(), str(tmp_path))
+    out = str(tmp_path / "fb.npy")
+    mp.spawn(_split_worker, args=(2, _free_port(), txt, W, H, spp, depth, out), nprocs=2, join=True)
+    got = np.load(out).reshape(-1, 3).astype(np.float64)
+    want = O.render(txt, W, H, spp, depth, order=O.ORDER_GROUP64).astype(np.float64)
+    rmse = np.sqrt(np.mean((got - want) ** 2, axis=0))
+    assert np.all(rmse < 1e-6), rmse
+    assert np.abs(got - want).max() <= 1e-6 * max(1.0, np.abs(want).max())

@@ -190,3 +190,81 @@ def test_round_cut_paths_bitexact(built, tmp_path, monkeypatch, cap):
     g = pt.render(root, W, H, spp, depth)
     o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_GROUP64)
     assert_bits(g, o, "PT_ROOM_CAP=%d" % cap)
+
+
+def test_c4_eight_shards_on_one_gpu(built, tmp_path):
+    """C4's per-rank work: the C3 frame at 1920x1080 cut into the
+    8 ranks' hashed 16x16 tile sets (pathtrace.dist.rank_pixels), each shard
+    rendered through `pixels=` as its rank would, the zero-filled per-rank
+    frames summed as the RCCL reduce does.  Bit-identical to the full frame,
+    and the shards' pixels bit-identical to the oracle on hashed pixels
+    (replaces the reference's block farm, src/test.cpp:520-778)."""
+    cfg = scenes.CONFIGS["C4"]
+    root = cfg.scene()
+    ds = pt.DeviceScene(root)
+    W, H, spp = cfg.width, cfg.height, 2
+    full = pt.render(ds, W, H, spp, cfg.depth, screen=cfg.screen).reshape(-1, 3)
+    acc = np.zeros_like(full)
+    owner = np.full(W * H, -1)
+    for r in range(8):
+        pix = ptdist.rank_pixels(W, H, r, 8)
+        owner[pix] = r
+        part = pt.render(ds, W, H, spp, cfg.depth, screen=cfg.screen, pixels=pix).reshape(-1, 3)
+        frame = np.zeros_like(full)
+        frame[pix] = part
+        acc = (acc + frame).astype(np.float32)
+    assert (owner >= 0).all()
+    assert_bits(acc, full, "8 shards summed vs full frame")
+    rng = np.random.default_rng(44)
+    pix = np.sort(rng.choice(W * H, 800, replace=False)).astype(np.int32)
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, cfg.depth, screen=cfg.screen, pixels=pix,
+                 order=O.ORDER_GROUP64)
+    assert_bits(acc[pix], o, "8 shards vs oracle")
+
+
+def test_sample_split_sums(built, tmp_path):
+    """bench.py's N-GPU sample split: a call renders samples sample_begin ..
+    sample_begin + spp - 1 of every pixel and (sum_only) writes their plain
+    sum in sample order; the oracle's per-sample values summed the same way
+    match bit for bit, and the ranks' sums added and divided by the total spp
+    stay within float rounding of the single-call frame."""
+    root = scenes.scene_p1()
+    W, H, S, depth = 40, 24, 12, 8
+    per = O.render(to_text(root, str(tmp_path)), W, H, S, depth, order=O.ORDER_GROUP64, per_sample=True)
+    ds = pt.DeviceScene(root)
+    total = np.zeros((W * H, 3), dtype=np.float32)
+    for b, c in [(0, 5), (5, 4), (9, 3)]:
+        g = pt.render(ds, W, H, c, depth, sample_begin=b, sum_only=True).reshape(-1, 3)
+        want = np.zeros((W * H, 3), dtype=np.float32)
+        for s in range(b, b + c):
+            want = (want + per[:, s]).astype(np.float32)
+        assert_bits(g, want, "samples %d..%d" % (b, b + c - 1))
+        total = (total + g).astype(np.float32)
+    full = pt.render(ds, W, H, S, depth).reshape(-1, 3)
+    e = rmse(total / np.float32(S), full)
+    assert np.all(e <= 1e-6), e
+
+
+@pytest.mark.parametrize("name", ["C3", "C2", "C5"])
+def test_config_scale_vs_reference(built, name):
+    """Each benchmark config at its real spp and depth against the UNMODIFIED
+    reference (tests/golden/config_*.npz, frozen by make_config_golden.py):
+    hashed pixels (C5: half on the skybox sphere), reference order bit for bit
+    (C5's spherical sky map calls atan2f/asinf, whose last-ulp differences from
+    glibc can move a texel: held to the RMSE bar instead), fast order within
+    RMSE 1e-5."""
+    z = np.load(os.path.join(GOLD, "config_%s.npz" % name))
+    pix, ref = z["pixels"], z["means"]
+    W, H, spp, depth, seed = [int(v) for v in z["meta"][:5]]
+    cfg = scenes.CONFIGS[name]
+    ds = pt.DeviceScene(cfg.scene())
+    g = pt.render(ds, W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix, order="reference")
+    if name == "C5":
+        e = rmse(g, ref)
+        assert np.all(e <= 1e-5), e
+        assert np.isclose(g, ref, rtol=1e-5, atol=1e-7).all(axis=1).mean() >= 0.95
+    else:
+        assert_bits(g, ref, "%s reference order vs ptref" % name)
+    f = pt.render(ds, W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix, order="fast")
+    e = rmse(f, ref)
+    assert np.all(e <= 1e-5), e

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Counter evidence for the bench line: three rocprofv3 --pmc passes of the
+# bench command itself (issue/busy counters, FETCH_SIZE, WRITE_SIZE -- never
+# combined with tracing), summarised by tools/pmc_summary.py into OUT/pmc.json.
+# usage: tools/pmc_bench.sh OUTDIR [bench args...]
+OUT=${1:-gpurun_out/pmcb}; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$OUT"; OUT=$(cd "$OUT" && pwd)
+cd /tmp && export TMPDIR=/tmp
+pass() {
+    name=$1; shift
+    timeout -k 10 600 rocprofv3 --pmc "$@" -d "$OUT/$name" -o $name --output-format csv -- python3 "$ROOT/bench.py" --no-cpu "${BENCH_ARGS[@]}" > "$OUT/$name.log" 2>&1
+    rc=$?; echo "$name rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+}
+BENCH_ARGS=("$@")
+pass busy SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/pmc.json" && cat "$OUT/pmc.json"

@@ -1,0 +1,58 @@
+"""Summarise tools/pmc_bench.sh: the render kernel's VALU/SALU busy fractions
+and HBM traffic under the bench command, per launch and per sample.
+
+VALUBusy follows rocprof's derived metric: SQ_ACTIVE_INST_VALU (quad-cycles
+summed over waves) x 4 / SIMDs / GRBM_GUI_ACTIVE per XCD (GRBM is summed over
+the 8 XCDs).  It counts one quad-cycle per VALU instruction, so it measures
+VALU issue occupancy, not lane utilisation.  HBM bytes: FETCH_SIZE doubled
+(gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md) + WRITE_SIZE,
+both in KB.  usage: pmc_summary.py OUTDIR"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+out = sys.argv[1]
+SIMDS, XCDS = 1024, 8
+
+
+def counters(name):
+    agg = collections.defaultdict(float)
+    n = 0
+    for f in glob.glob("%s/%s/**/*counter_collection.csv" % (out, name), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Kernel_Name"].startswith("pt_render_fast"):
+                agg[r["Counter_Name"]] += float(r["Counter_Value"])
+                n += 1
+    return agg
+
+
+def bench_line(name):
+    for line in open("%s/%s.log" % (out, name)):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise SystemExit("no bench line in %s.log" % name)
+
+
+busy, fetch, write = counters("busy"), counters("fetch"), counters("write")
+b = bench_line("busy")
+launches = b["steps"]  # one render launch per step at the bench config (one pass)
+samples = b["value"] * 1e6 * b["ms_per_step"] * 1e-3 * b["steps"]
+kernel_s = b["roofline"]["avg_launch_ms"] * 1e-3 if "roofline" in b else None
+gui = busy["GRBM_GUI_ACTIVE"] / XCDS
+res = {
+    "kernel": "pt_render_fast", "workload": b["config"]["workload"], "bench_value": b["value"],
+    "valu_busy": busy["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / gui,
+    "salu_busy": busy["SQ_ACTIVE_INST_SCA"] * 4 / SIMDS / gui,
+    "valu_insts_per_sample": busy["SQ_INSTS_VALU"] / samples,
+    "salu_insts_per_sample": busy["SQ_INSTS_SALU"] / samples,
+    "wave_cycles_per_sample": 4 * busy["SQ_WAVE_CYCLES"] / samples,
+    "fetch_bytes_per_launch": 2 * 1024 * fetch["FETCH_SIZE"] / launches,
+    "write_bytes_per_launch": 1024 * write["WRITE_SIZE"] / launches,
+}
+res["hbm_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
+res["hbm_bytes_per_sample"] = res["hbm_bytes_per_launch"] * launches / samples
+if kernel_s:
+    res["hbm_GBps"] = res["hbm_bytes_per_launch"] / kernel_s / 1e9
+print(json.dumps(res, indent=1))

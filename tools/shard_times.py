@@ -1,0 +1,40 @@
+"""Per-rank kernel time of a sharded config on ONE GPU: renders
+each rank's hashed 16x16 tile set (pathtrace.dist.rank_pixels) at the config's
+full spp, one after the other, and reports each shard's kernel time.  The
+slowest shard bounds a real N-GPU run (every rank renders its shard, then one
+reduce), so max/mean is the load-imbalance factor and N * mean / max the
+scaling ceiling the partition leaves.  usage: shard_times.py [C4] [world] [spp]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "path-trace_amd"))
+import pathtrace as pt  # noqa: E402
+from pathtrace import dist as ptdist  # noqa: E402
+from pathtrace import scenes  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "C4"
+cfg = scenes.CONFIGS[name]
+world = int(sys.argv[2]) if len(sys.argv) > 2 else cfg.gpus
+spp = int(sys.argv[3]) if len(sys.argv) > 3 else cfg.spp
+ds = pt.DeviceScene(cfg.scene())
+rows = []
+for r in range(world):
+    pix = ptdist.rank_pixels(cfg.width, cfg.height, r, world)
+    t = time.time()
+    _, st = pt.render(ds, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, pixels=pix, stats=True,
+                      max_buffer_bytes=40 << 30)  # one pass per shard, as bench.py
+    rows.append({"rank": r, "pixels": int(len(pix)), "kernel_ms": st["kernel_ms"], "reduce_ms": st["reduce_ms"],
+                 "launches": st["launches"], "queries_per_sample": st["queries"] / st["samples"],
+                 "wall_s": time.time() - t})
+    print(json.dumps(rows[-1]), flush=True)
+k = np.array([x["kernel_ms"] for x in rows])
+samples = cfg.width * cfg.height * spp
+print(json.dumps({"config": name, "world": world, "spp": spp, "max_ms": float(k.max()), "mean_ms": float(k.mean()),
+                  "imbalance_max_over_mean": float(k.max() / k.mean()),
+                  "scaling_ceiling": float(world * k.mean() / k.max()),
+                  "Msamples_per_s_if_parallel": samples / k.max() / 1e3}), flush=True)
