@@ -235,6 +235,7 @@ def main():
                     "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE, %s)" %
                                     os.path.relpath(PMC_JSON % cfg.name, ROOT),
                     "valu_busy": round(ev["valu_busy"], 4), "salu_busy": round(ev["salu_busy"], 4),
+                    "valu_insts_per_simd_cycle": round(ev.get("valu_insts_per_simd_cycle", 0), 4),
                     "hbm_GBps": round(ev["hbm_GBps"], 2), "hbm_peak_GBps": 8000.0})
         if not args.no_cpu and world == 1:
             try:

@@ -44,6 +44,10 @@ gui = busy["GRBM_GUI_ACTIVE"] / XCDS
 res = {
     "kernel": "pt_render_fast", "workload": b["config"]["workload"], "bench_value": b["value"],
     "valu_busy": busy["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / gui,
+    # > 1 on gfx950: more than one VALU instruction is active per quad-cycle
+    # per SIMD (co-issue), so also report the issue rate itself
+    "valu_insts_per_simd_cycle": busy["SQ_INSTS_VALU"] / SIMDS / gui,
+    "salu_insts_per_simd_cycle": busy["SQ_INSTS_SALU"] / SIMDS / gui,
     "salu_busy": busy["SQ_ACTIVE_INST_SCA"] * 4 / SIMDS / gui,
     "valu_insts_per_sample": busy["SQ_INSTS_VALU"] / samples,
     "salu_insts_per_sample": busy["SQ_INSTS_SALU"] / samples,
