@@ -70,6 +70,8 @@ struct PtLaunch
     int gw;             /* pixel index = py * gw + px (gw = W, or wider for the
                            adaptive caller's block-edge pixels)                   */
     int chunk;          /* items per work-queue dequeue, 1..64 (0 = PT_CHUNK)      */
+    int sample_major;   /* item order: 1 = consecutive items are consecutive slots
+                           at one sample, 0 = a slot's samples are consecutive    */
 };
 
 struct Env
@@ -2384,6 +2386,28 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
 #ifndef PT_WPW
 #define PT_WPW 4 /* independent waves per workgroup */
 #endif
+/* Work item -> (pixel slot, sample).  Sample-major (small launches, chosen
+ * by the runtime): consecutive items are consecutive slots at one sample, so
+ * a dequeued chunk holds one sample of each of CH neighbouring pixels and an
+ * expensive pixel's samples spread over many chunks -- slot-major chunks
+ * hold up to CH samples of one pixel, and one wave could draw hundreds of ms
+ * of work near the end of a launch (C3 at 16 spp: 73 Msamples/s slot-major,
+ * 98 sample-major).  Large launches stay slot-major: their last chunks are
+ * the frame's last pixels, a short tail (C3 at 128 spp: sample-major -2 %).
+ * Results do not depend on the order: every (pixel, sample) is seeded by its
+ * own indices and the stage buffer is indexed slot-major either way. */
+__device__ __forceinline__ void item_slot(const PtLaunch &lp, long long item, long long &slot, int &s)
+{
+    if (lp.sample_major) {
+        const long long nslots = lp.n_items / lp.nsamp;
+        const long long k = item / nslots;
+        slot = item - k * nslots;
+        s = lp.s0 + (int)k;
+    } else {
+        slot = item / lp.nsamp;
+        s = lp.s0 + (int)(item - slot * lp.nsamp);
+    }
+}
 #ifndef PT_CHUNK
 #define PT_CHUNK 32 /* default (pixel, sample) items a wave takes per dequeue (<= 64) */
 #endif
@@ -2437,8 +2461,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         V3 lres = mk(0, 0, 0);
         if (lane < CH && item0 + lane < lp.n_items) {
             const long long item = item0 + lane;
-            const long long slot = item / lp.nsamp;
-            const int s = lp.s0 + (int)(item - slot * lp.nsamp);
+            long long slot;
+            int s;
+            item_slot(lp, item, slot, s);
             const int pix = pixels ? pixels[slot] : (int)slot;
             Rng r;
             rng_seed(r, lp.seed, (u64)pix, (u64)s);
@@ -2462,8 +2487,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             const long long item = item0 + j;
             if (item >= lp.n_items)
                 break;
-            const long long slot = item / lp.nsamp;
-            const int s = lp.s0 + (int)(item - slot * lp.nsamp);
+            long long slot;
+            int s;
+            item_slot(lp, item, slot, s);
             const int pix = pixels ? pixels[slot] : (int)slot;
             if ((DONE >> j) & 1ull)
                 continue;
@@ -2477,9 +2503,13 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         }
         const long long my = item0 + lane;
         if (lane < CH && my < lp.n_items) {
-            out[3 * my + 0] = mine.x;
-            out[3 * my + 1] = mine.y;
-            out[3 * my + 2] = mine.z;
+            long long slot;
+            int s;
+            item_slot(lp, my, slot, s);
+            const long long st = slot * lp.nsamp + (s - lp.s0); /* the stage stays slot-major for pt_reduce */
+            out[3 * st + 0] = mine.x;
+            out[3 * st + 1] = mine.y;
+            out[3 * st + 2] = mine.z;
         }
     }
     if (lane == 0) {

@@ -66,6 +66,7 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     int nsamp;
     int s0;
     int gw, chunk;
+    int sample_major;
 };
 
 template <class T>
@@ -596,6 +597,9 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             lp.s0 = p->sample_begin + s0;
             lp.gw = p->grid_width > 0 ? p->grid_width : p->width;
             lp.chunk = chunk;
+            /* sample-major item order for launches of up to 64 samples per slot
+             * (pt_device.h item_slot) */
+            lp.sample_major = nsamp <= 64 ? 1 : 0;
             const float *Pp = ds.P.p;
             const PtImageDev *ip = ds.imgs.p;
             const uint64_t *jp = ds.jump.p;
