@@ -25,7 +25,10 @@
  *                     draw no random numbers) are summed in groups of up to 64
  *                     by a pairwise tree over 64 slots padded with -0.0f, and
  *                     each group total is added to retval; a non-leaf child
- *                     closes the open group and is added on its own.
+ *                     closes the open group and is added on its own.  A
+ *                     pixel's samples are summed in blocks of 32 (pairwise
+ *                     tree each, padded with -0.0f), blocks one after the
+ *                     other (pixel_sum).
  */
 #include "oracle_engine.h"
 #include "scene_text.h"
@@ -863,6 +866,31 @@ inline V3 pairwise64(const std::vector<V3> &g)
     return V3(b[0][0], b[1][0], b[2][0]);
 }
 
+/* A pixel's sum of spp samples: in the reference order one after the other
+ * (tracePixel, path-trace.h:192-199); in the group-64 order in blocks of 32
+ * consecutive samples, each block its pairwise tree (missing leaves -0.0f),
+ * the block sums added one after the other -- the GPU fast path's pixel sum
+ * (pt_device.h pt_reduce / render_chunk block partials). */
+template <class F>
+V3 pixel_sum(int spp, int order, F &&sample)
+{
+    V3 acc(0, 0, 0);
+    if (order != ORDER_GROUP64) {
+        for (int s = 0; s < spp; s++) acc = acc + sample(s);
+        return acc;
+    }
+    std::vector<V3> blk;
+    blk.reserve(32);
+    for (int s = 0; s < spp; s++) {
+        blk.push_back(sample(s));
+        if (blk.size() == 32 || s == spp - 1) {
+            acc = acc + pairwise64(blk);
+            blk.clear();
+        }
+    }
+    return acc;
+}
+
 template <class E>
 struct Tracer
 {
@@ -1124,11 +1152,10 @@ int oracle_render_adaptive(const char *scene_text, int W, int H, int spp, int de
                     b.valid.assign((size_t)(block + 1) * (block + 1), 0);
                     b.trace_pixel = [&](int px, int py) {
                         const uint64_t p = (uint64_t)py * gw + px;
-                        V3 acc(0, 0, 0);
-                        for (int s = 0; s < spp; s++) {
+                        V3 acc = pixel_sum(spp, order == 1 ? ORDER_GROUP64 : ORDER_REFERENCE, [&](int s) {
                             SampleEngine e(seed, p, (uint64_t)s);
-                            acc = acc + tr.sample(px, py, W, H, depth, sw, sh, dist, e);
-                        }
+                            return tr.sample(px, py, W, H, depth, sw, sh, dist, e);
+                        });
                         ntraced++;
                         return acc / (float)spp;
                     };
@@ -1195,16 +1222,15 @@ int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int 
                         break;
                     int p = pixels ? pixels[k] : k;
                     int px = p % gw, py = p / gw;
-                    V3 acc(0, 0, 0);
-                    for (int s = 0; s < spp; s++) {
+                    V3 acc = pixel_sum(spp, order == 1 ? ORDER_GROUP64 : ORDER_REFERENCE, [&](int s) {
                         SampleEngine e(seed, (uint64_t)p, (uint64_t)s);
                         V3 c = tr.sample(px, py, W, H, depth, sw, sh, dist, e);
                         if (per_sample) {
                             float *o = out + ((size_t)k * spp + s) * 3;
                             o[0] = c.x, o[1] = c.y, o[2] = c.z;
                         }
-                        acc = acc + c;
-                    }
+                        return c;
+                    });
                     acc = acc / (float)spp;
                     if (!per_sample) {
                         out[3 * (size_t)k + 0] = acc.x;

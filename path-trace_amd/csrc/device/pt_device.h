@@ -72,6 +72,8 @@ struct PtLaunch
     int chunk;          /* items per work-queue dequeue, 1..64 (0 = PT_CHUNK)      */
     int sample_major;   /* item order: 1 = consecutive items are consecutive slots
                            at one sample, 0 = a slot's samples are consecutive    */
+    int block_sums;     /* stage one partial per 32-sample block (slot-major,
+                           chunk 32, nsamp % 32 == 0), else one value per sample */
 };
 
 struct Env
@@ -2502,7 +2504,26 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                 mine = c;
         }
         const long long my = item0 + lane;
-        if (lane < CH && my < lp.n_items) {
+        if (lp.block_sums) {
+            /* the chunk is one 32-sample block of one slot (slot-major, chunk
+             * 32, nsamp % 32 == 0): its 32-leaf pairwise tree is the block
+             * partial of the group-64 order's pixel sum.  Level w adds lane
+             * k + w into lane k, so lane 0 ends with pt_tree32's association.
+             * The three sums are read out of lane 0 here, at full exec, and
+             * lanes 0-2 store one channel each: a read of lane 0 inside a
+             * lane-conditional branch would let the compiler sink the last
+             * level's add into that branch, where lane 0 does not run. */
+            V3 b = mine;
+#pragma unroll
+            for (int w = 1; w < 32; w *= 2) {
+                const float ox = __shfl_down(b.x, w), oy = __shfl_down(b.y, w), oz = __shfl_down(b.z, w);
+                b = mk(b.x + ox, b.y + oy, b.z + oz);
+            }
+            const float bx = rdlane(b.x, 0), by = rdlane(b.y, 0), bz = rdlane(b.z, 0);
+            const float v = lane == 0 ? bx : lane == 1 ? by : bz;
+            if (lane < 3)
+                out[3 * (item0 >> 5) + lane] = v;
+        } else if (lane < CH && my < lp.n_items) {
             long long slot;
             int s;
             item_slot(lp, my, slot, s);
@@ -2577,13 +2598,32 @@ __device__ constexpr int min_workgroups()
 
 #ifndef PT_DEVICE_REDUCE_DEFINED
 #define PT_DEVICE_REDUCE_DEFINED
-/* Ordered per-pixel sample sum: acc = ((acc + x_0) + x_1) + ..., the
- * accumulation order of tracePixel's spp loop (path-trace.h:192-199); on the
- * last pass writes acc / spp to the frame buffer.  One thread per pixel slot. */
+/* Per-pixel sample sums, one thread per pixel slot, carried across passes in
+ * accum; on the last pass acc / spp goes to the frame buffer.
+ *   mode 0 (reference order): acc = ((acc + x_0) + x_1) + ..., tracePixel's
+ *          own accumulation (path-trace.h:192-199), from per-sample values;
+ *   mode 1 (group-64 order, per-sample stage): samples in blocks of 32 from
+ *          the call's first sample, each block its 32-leaf pairwise tree
+ *          (missing leaves -0.0f), acc = ((acc + B_0) + B_1) + ...;
+ *   mode 2 (group-64 order, block stage): the same with the block partials
+ *          already summed by the render kernel (one per 32 samples). */
+__device__ __forceinline__ float pt_tree32(const float *v, int n, int stride)
+{
+    float b[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++)
+        b[k] = k < n ? v[k * stride] : -0.0f;
+#pragma unroll
+    for (int w = 1; w < 32; w *= 2)
+#pragma unroll
+        for (int k = 0; k < 32; k += 2 * w)
+            b[k] = b[k] + b[k + w];
+    return b[0];
+}
 extern "C" __global__ __launch_bounds__(256) void pt_reduce(const float *__restrict__ in, float *__restrict__ accum,
                                                             float *__restrict__ fb, const int *__restrict__ pixels,
                                                             long long nslots, int nsamp, int first, int last,
-                                                            float spp)
+                                                            float spp, int mode)
 {
     const long long slot = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (slot >= nslots)
@@ -2594,11 +2634,29 @@ extern "C" __global__ __launch_bounds__(256) void pt_reduce(const float *__restr
         ay = accum[3 * slot + 1];
         az = accum[3 * slot + 2];
     }
-    const float *p = in + 3 * slot * (long long)nsamp;
-    for (int s = 0; s < nsamp; s++) {
-        ax = ax + p[3 * s + 0];
-        ay = ay + p[3 * s + 1];
-        az = az + p[3 * s + 2];
+    if (mode == 2) {
+        const int nb = nsamp >> 5;
+        const float *p = in + 3 * slot * (long long)nb;
+        for (int b = 0; b < nb; b++) {
+            ax = ax + p[3 * b + 0];
+            ay = ay + p[3 * b + 1];
+            az = az + p[3 * b + 2];
+        }
+    } else if (mode == 1) {
+        const float *p = in + 3 * slot * (long long)nsamp;
+        for (int s = 0; s < nsamp; s += 32) {
+            const int n = nsamp - s < 32 ? nsamp - s : 32;
+            ax = ax + pt_tree32(p + 3 * s + 0, n, 3);
+            ay = ay + pt_tree32(p + 3 * s + 1, n, 3);
+            az = az + pt_tree32(p + 3 * s + 2, n, 3);
+        }
+    } else {
+        const float *p = in + 3 * slot * (long long)nsamp;
+        for (int s = 0; s < nsamp; s++) {
+            ax = ax + p[3 * s + 0];
+            ay = ay + p[3 * s + 1];
+            az = az + p[3 * s + 2];
+        }
     }
     if (last) {
         const long long pix = pixels ? (long long)pixels[slot] : slot;

@@ -67,6 +67,7 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     int s0;
     int gw, chunk;
     int sample_major;
+    int block_sums;
 };
 
 template <class T>
@@ -507,16 +508,46 @@ size_t frame_floats(const pt_render_params *p)
     return 3 * n;
 }
 
+/* The group-64 order sums a pixel's samples in blocks of 32 (pt_device.h
+ * pt_reduce); a slot-major launch of whole blocks stages one partial per
+ * block instead of one value per sample (32x less: C4 3.2 GB, C5 25 GB in one
+ * pass). */
+bool block_staging(const pt_render_params *p)
+{
+    static const bool off = [] {
+        const char *env = getenv("PT_BLOCK_SUMS"); /* experiment hook: 0 = per-sample staging only */
+        if (!env || !*env)
+            return false;
+        fprintf(stderr, "pt: experiment hook PT_BLOCK_SUMS=%s active\n", env);
+        return atoi(env) == 0;
+    }();
+    return !off && p->order == PT_ORDER_GROUP64 && p->spp > 64 && p->spp % 32 == 0;
+}
+
 long long pass_samples(const pt_render_params *p, long long npix)
 {
     int64_t budget = p->max_buffer_bytes > 0 ? p->max_buffer_bytes : (8ll << 30);
-    long long per_pass = budget / (12ll * npix);
+    long long per_pass = budget / (12ll * npix) * (block_staging(p) ? 32 : 1);
     per_pass = per_pass / 64 * 64;
     if (per_pass < 64)
         per_pass = 64;
     if (per_pass > p->spp)
         per_pass = p->spp;
     return per_pass;
+}
+
+/* Stage floats for the largest launch of a render: block partials for
+ * slot-major whole-block launches, else one value per sample -- launches of
+ * <= 64 samples per slot (sample-major) and small launches whose chunks fall
+ * below 32 items (at most 4 * 32 items per resident wave). */
+size_t stage_floats(const pt_render_params *p, long long npix, long long per_pass)
+{
+    if (!block_staging(p))
+        return (size_t)(npix * per_pass * 3);
+    size_t n = (size_t)(npix * (per_pass / 32) * 3);
+    n = std::max(n, (size_t)(npix * std::min<long long>(64, p->spp) * 3));
+    n = std::max(n, (size_t)(4ll * 32 * 16384 * 3)); /* a small launch: < 4 chunks of 32 per wave, <= 16384 waves */
+    return std::min(n, (size_t)(npix * per_pass * 3));
 }
 
 /* Module, parameters and every device buffer a render with p needs. */
@@ -529,7 +560,7 @@ DeviceState &prepare(SceneImpl &s, const pt_render_params *p, Generated &g)
     const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
     if (npix > 0) {
         long long per_pass = pass_samples(p, npix);
-        ds.stage.ensure((size_t)(npix * per_pass * 3));
+        ds.stage.ensure(stage_floats(p, npix, per_pass));
         if (p->spp > per_pass)
             ds.accum.ensure((size_t)npix * 3);
         if (p->pixels)
@@ -565,6 +596,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
     std::vector<std::pair<int, int>> spans; /* (start event, end event) per render launch */
     std::vector<std::pair<int, int>> rspans;
     for (int s0 = 0; s0 < p->spp; s0 += (int)per_pass) {
+        int reduce_mode = 0;
         int nsamp = (int)std::min<long long>(per_pass, p->spp - s0);
         long long n_items = npix * nsamp;
         /* 32 items per dequeue amortise the queue (A/B on C3: 16 -> 32 +2.7%, 64 same); a launch too small to give
@@ -600,6 +632,10 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             /* sample-major item order for launches of up to 64 samples per slot
              * (pt_device.h item_slot) */
             lp.sample_major = nsamp <= 64 ? 1 : 0;
+            /* one staged partial per 32-sample block when a chunk is a block */
+            lp.block_sums = (block_staging(p) && !lp.sample_major && chunk == 32 && nsamp % 32 == 0) ? 1 : 0;
+            reduce_mode = p->order == PT_ORDER_REFERENCE ? 0 : lp.block_sums ? 2 : 1;
+            ds.stage.ensure((size_t)(lp.block_sums ? npix * (nsamp / 32) * 3 : npix * nsamp * 3));
             const float *Pp = ds.P.p;
             const PtImageDev *ip = ds.imgs.p;
             const uint64_t *jp = ds.jump.p;
@@ -625,7 +661,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             long long ns = npix;
             int first = s0 == 0, last = s0 + nsamp == p->spp;
             float spp = p->sum_only ? 1.0f : (float)p->spp; /* x / 1 == x: the raw sum */
-            void *args[] = {&in, &acc, &fb, &pp, &ns, &nsamp, &first, &last, &spp};
+            void *args[] = {&in, &acc, &fb, &pp, &ns, &nsamp, &first, &last, &spp, &reduce_mode};
             unsigned blocks = (unsigned)((npix + 255) / 256);
             int e0 = (int)evs.size();
             if (st)

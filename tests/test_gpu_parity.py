@@ -39,6 +39,26 @@ def golden_means(name):
     return (acc / np.float32(ps.shape[1])).astype(np.float32)
 
 
+def tree32(v):
+    """pairwise tree of up to 32 float32 rows (n x 3), missing leaves -0.0f"""
+    b = np.full((32,) + v.shape[1:], -0.0, dtype=np.float32)
+    b[:len(v)] = v
+    w = 1
+    while w < 32:
+        b[0:32:2 * w] = (b[0:32:2 * w] + b[w:32:2 * w]).astype(np.float32)
+        w *= 2
+    return b[0]
+
+
+def block_sum(per):
+    """the group-64 order's pixel sum of per-sample values (npx x n x 3):
+    blocks of 32 samples, pairwise tree each, blocks added in order"""
+    acc = np.zeros((per.shape[0], 3), dtype=np.float32)
+    for s in range(0, per.shape[1], 32):
+        acc = (acc + np.stack([tree32(px[s:s + 32]) for px in per])).astype(np.float32)
+    return acc
+
+
 def assert_bits(gpu, ref, what):
     gpu = np.ascontiguousarray(gpu, dtype=np.float32).reshape(-1, 3)
     ref = np.ascontiguousarray(ref, dtype=np.float32).reshape(-1, 3)
@@ -224,10 +244,12 @@ def test_c4_eight_shards_on_one_gpu(built, tmp_path):
 
 def test_sample_split_sums(built, tmp_path):
     """bench.py's N-GPU sample split: a call renders samples sample_begin ..
-    sample_begin + spp - 1 of every pixel and (sum_only) writes their plain
-    sum in sample order; the oracle's per-sample values summed the same way
-    match bit for bit, and the ranks' sums added and divided by the total spp
-    stay within float rounding of the single-call frame."""
+    sample_begin + spp - 1 of every pixel and (sum_only) writes their sum in
+    the group-64 order's pixel order (blocks of 32 from the call's first
+    sample, pairwise tree each, blocks in order); the oracle's per-sample
+    values summed the same way match bit for bit, and the ranks' sums added
+    and divided by the total spp stay within float rounding of the
+    single-call frame."""
     root = scenes.scene_p1()
     W, H, S, depth = 40, 24, 12, 8
     per = O.render(to_text(root, str(tmp_path)), W, H, S, depth, order=O.ORDER_GROUP64, per_sample=True)
@@ -235,9 +257,7 @@ def test_sample_split_sums(built, tmp_path):
     total = np.zeros((W * H, 3), dtype=np.float32)
     for b, c in [(0, 5), (5, 4), (9, 3)]:
         g = pt.render(ds, W, H, c, depth, sample_begin=b, sum_only=True).reshape(-1, 3)
-        want = np.zeros((W * H, 3), dtype=np.float32)
-        for s in range(b, b + c):
-            want = (want + per[:, s]).astype(np.float32)
+        want = block_sum(per[:, b:b + c])
         assert_bits(g, want, "samples %d..%d" % (b, b + c - 1))
         total = (total + g).astype(np.float32)
     full = pt.render(ds, W, H, S, depth).reshape(-1, 3)
@@ -246,13 +266,17 @@ def test_sample_split_sums(built, tmp_path):
 
 
 @pytest.mark.parametrize("name", ["C3", "C2", "C5"])
-def test_config_scale_vs_reference(built, name):
+def test_config_scale_vs_reference(built, name, tmp_path):
     """Each benchmark config at its real spp and depth against the UNMODIFIED
     reference (tests/golden/config_*.npz, frozen by make_config_golden.py):
     hashed pixels (C5: half on the skybox sphere), reference order bit for bit
     (C5's spherical sky map calls atan2f/asinf, whose last-ulp differences from
     glibc can move a texel: held to the RMSE bar instead), fast order within
-    RMSE 1e-5."""
+    RMSE 1e-5 -- except C5, whose 8192-sample pixel sums the reference adds
+    sequentially: there the reference itself is 3.9e-5 RMSE from the float64
+    mean and the fast order's 32-sample blocks 5e-7, so the fast
+    order is held to the oracle's group-64 order at 1e-5 and to the reference
+    at 1e-4 (the north star's bar is 1e-3)."""
     z = np.load(os.path.join(GOLD, "config_%s.npz" % name))
     pix, ref = z["pixels"], z["means"]
     W, H, spp, depth, seed = [int(v) for v in z["meta"][:5]]
@@ -266,5 +290,37 @@ def test_config_scale_vs_reference(built, name):
     else:
         assert_bits(g, ref, "%s reference order vs ptref" % name)
     f = pt.render(ds, W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix, order="fast")
+    bar = 1e-5
+    if name == "C5":
+        o = O.render(to_text(cfg.scene(), str(tmp_path)), W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix,
+                     order=O.ORDER_GROUP64)
+        e = rmse(f, o)
+        assert np.all(e <= 1e-5), e
+        assert np.isclose(f, o, rtol=1e-5, atol=1e-7).all(axis=1).mean() >= 0.95
+        bar = 1e-4
     e = rmse(f, ref)
-    assert np.all(e <= 1e-5), e
+    assert np.all(e <= bar), e
+
+
+def test_block_staged_pixel_sums(built, tmp_path):
+    """Slot-major launches of whole 32-sample blocks (chunks of 32, >= 4 per
+    resident wave) stage one partial per block, the chunk's 32 samples summed
+    by the DPP tree; passes of 64 samples stage per-sample values and pt_reduce
+    forms the blocks.  Both bit-identical to each other on every pixel and to
+    the oracle's group-64 order (and a numpy restatement of the pixel sum) on
+    hashed pixels."""
+    root = scenes.scene_p1()
+    W, H, spp, depth = 256, 160, 128, 8
+    ds = pt.DeviceScene(root)
+    one, st1 = pt.render(ds, W, H, spp, depth, stats=True)
+    # a budget of 2 floats x 3 per pixel = 64 samples per pass under block staging
+    passes, st2 = pt.render(ds, W, H, spp, depth, max_buffer_bytes=W * H * 12 * 2, stats=True)
+    assert st1["launches"] == 1 and st2["launches"] == 2
+    assert_bits(one, passes, "block-staged vs per-sample passes")
+    rng = np.random.default_rng(3)
+    pix = np.sort(rng.choice(W * H, 300, replace=False)).astype(np.int32)
+    txt = to_text(root, str(tmp_path))
+    o = O.render(txt, W, H, spp, depth, pixels=pix, order=O.ORDER_GROUP64)
+    per = O.render(txt, W, H, spp, depth, pixels=pix, order=O.ORDER_GROUP64, per_sample=True)
+    assert_bits(block_sum(per) / np.float32(spp), o, "numpy block sums vs oracle")
+    assert_bits(one.reshape(-1, 3)[pix], o, "block-staged vs oracle")
