@@ -6,11 +6,14 @@ reference CPU renderer on a hashed pixel subset.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
 
-One step = one full frame: every rank renders the 16x16 tiles it owns
-(pathtrace.dist) into a zeroed full-frame float3 buffer with the HIP
-megakernel (libpt.so, C ABI) and the frames are sum-reduced to rank 0 over
-RCCL; the timed region is bracketed by barrier + device synchronise and the
-max over ranks is reported.  Inputs (the scene) are resident before timing.
+One step = one full frame.  N = 1: the HIP megakernel (libpt.so, C ABI)
+renders every pixel into a device frame buffer.  N > 1 (--split samples, the
+default): every rank renders every pixel for its share of the samples
+(sample_begin / sum_only), the per-pixel sums are reduced to rank 0 over RCCL
+and divided by spp; --split tiles: every rank renders the hashed 16x16 tiles
+it owns (pathtrace.dist) and the disjoint frames are sum-reduced.  The timed
+region is bracketed by barrier + device synchronise and the max over ranks is
+reported.  Inputs (the scene) are resident before timing.
 
 Extra fields: `roofline` (VALU-bound: the SURVEY.md s8(d) FP32 op model per
 root query x the kernel's exact query count / HIP-event kernel time, against
@@ -34,17 +37,19 @@ sys.path[:0] = [os.path.join(ROOT, "path-trace_amd"), os.path.join(ROOT, "oracle
 
 VALU_PEAK_TOPS = 78.6  # 256 CU x 128 FP32 lanes/clk x 2.4 GHz, no FMA (contraction off for parity)
 # SURVEY.md s8(d) op model calibrated by tools/calibrate_ops.py (oracle event
-# counts on hashed pixels): C3 8192 px x 32 spp, C2 512 px x 4 spp
-OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 614.78}
+# counts on hashed pixels): C3 8192 px x 32 spp, C2 512 px x 4 spp, C5 8192 px x 64 spp
+# (C5's texture work -- spherical/skybox maps -- is outside the op model)
+OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 614.78, "C5": 554.13}
 # Counter evidence of this same command (tools/pmc_bench.sh: rocprofv3 --pmc
 # passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 + WRITE_SIZE)
 PMC_JSON = os.path.join(ROOT, "profiles", "round2", "pmc_bench_%s.json")
 # bounded CPU samples (~10-30 s of reference work on the box's 16 host threads)
-CPU_PIXELS = {"C1": 2048, "C2": 512, "C3": 2048, "C4": 2048, "C5": 64}
+CPU_PIXELS = {"C1": 2048, "C2": 512, "C3": 2048, "C4": 2048, "C5": 32768}
 # C5 (3840x2160 x 8192 spp, 68 G samples) is timed on a hashed pixel subset at
 # its full spp and depth: at that size the reference camera (|d| = 4320) hides
-# everything nearer than 4.32 units, so the frame is the sky box and the skybox
-# sphere and per-pixel cost is uniform enough for a subset to represent it
+# everything nearer than 4.32 units, so the frame is the sky box, the skybox
+# sphere and the far side of the glass ball (~6 % of pixels, ~60x the cost of a
+# sky pixel); a hashed subset of 65536 pixels holds the same mix
 SUBSET = {"C5": 65536}
 
 
@@ -151,7 +156,7 @@ def main():
     spp = args.spp or cfg.spp
     W, H = cfg.width, cfg.height
     root = cfg.scene()
-    ds = pt.DeviceScene(root)
+    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu)
     subset = SUBSET.get(cfg.name, 0) if args.subset < 0 else args.subset
     by_samples = world > 1 and args.split == "samples"
     mine = ptdist.rank_pixels(W, H, rank, 1 if by_samples else world)

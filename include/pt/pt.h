@@ -197,6 +197,13 @@ int pt_prepare(pt_scene *s, const pt_render_params *p);
  * scene and depth without touching a GPU.  Used by build() to pre-populate the
  * in-tree cache. */
 int pt_scene_compile(pt_scene *s, int depth);
+/* MI355X tuning knob, no reference counterpart: build this scene's megakernel
+ * for 1..5 resident workgroups (of 4 waves) per CU instead of the most its
+ * LDS allows (0 = auto).  Fewer workgroups raise the VGPR cap (5: 96, 4: 128,
+ * 3: 168, 2: 256): scenes whose CSG tree spills at the default cap and whose
+ * samples are mostly spine walks run faster (C5: 2.3x at 2), burst-bound
+ * scenes slower (C2 at 2: -8 %).  Takes effect at the next compile/render. */
+int pt_scene_set_occupancy(pt_scene *s, int workgroups_per_cu);
 /* Key of the code object for this scene/depth (hex string, static storage). */
 const char *pt_scene_kernel_key(pt_scene *s, int depth);
 

@@ -237,6 +237,9 @@ Generated generate(const SceneImpl &s, int depth)
             src << "#define " << (eq == std::string::npos ? d : d.substr(0, eq) + " " + d.substr(eq + 1)) << "\n";
         }
     }
+    /* per-scene occupancy (pt_scene_set_occupancy): the launch bounds' workgroups per CU */
+    if (s.wg_per_cu > 0)
+        src << "#define PT_MIN_WAVES " << s.wg_per_cu << "\n";
     /* experiment hook: A/B a different device library text in the same run,
      * e.g. PT_DEVICE_HEADER=tools/ab/old.h (profiling only) */
     if (const char *hdr = getenv("PT_DEVICE_HEADER")) {

@@ -2265,9 +2265,15 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
             if (sp == 0) {
                 found = cam.hit != 0, t = cam.t, ref = cam.ref, ex = cam.ex != 0;
             } else {
+#ifdef PT_SPINE_TIMING
+                PT_T0(tq);
+#endif
                 typename S::Root::Ctx ctx;
                 S::Root::prep(ctx, o, e);
                 found = first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+#ifdef PT_SPINE_TIMING
+                PT_ACC(cnt, 0, tq);
+#endif
             }
             if (!found) {
                 result = mk(0, 0, 0);
@@ -2290,7 +2296,13 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 n = nn;
                 ior = (float)(1.0 / (double)S::ior(mat, e));
             }
+#ifdef PT_SPINE_TIMING
+            PT_T0(tm);
+#endif
             const V3 retval = S::emis(mat, hit, e);
+#ifdef PT_SPINE_TIMING
+            PT_ACC(cnt, 1, tm);
+#endif
             f.hit = hit, f.n = n, f.mat = mat, f.retval = retval, f.add = 1.0f;
             const float strength = unif(f.strength);
             if (uni(f.depth) <= 0 || strength < EPS) {
@@ -2299,7 +2311,13 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 continue;
             }
             cnt.shaded++;
+#ifdef PT_SPINE_TIMING
+            PT_T0(tr0);
+#endif
             const float rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
+#ifdef PT_SPINE_TIMING
+            PT_ACC(cnt, 2, tr0);
+#endif
             f.rf = rf;
             if (rf > EPS) {
                 V3 rd = refract(d, ior, n);
@@ -2460,13 +2478,16 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         /* the chunk's camera queries, one per lane */
         CamHit ch = {0, 0.0f, 0u, 0};
         int ldone = 0, lq = 0, lsh = 0;
+        int lpix = 0, ls = 0; /* the lane's (pixel, sample), read by the wave loop below */
         V3 lres = mk(0, 0, 0);
-        if (lane < CH && item0 + lane < lp.n_items) {
+        const bool lvalid = lane < CH && item0 + lane < lp.n_items;
+        if (lvalid) {
             const long long item = item0 + lane;
             long long slot;
             int s;
             item_slot(lp, item, slot, s);
             const int pix = pixels ? pixels[slot] : (int)slot;
+            lpix = pix, ls = s;
             Rng r;
             rng_seed(r, lp.seed, (u64)pix, (u64)s);
             const V3 d = camera_dir(lp, pix, r);
@@ -2483,22 +2504,18 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             cnt.queries += (u64)(__popcll(D) + __popcll(Q2));
             cnt.shaded += (u64)__popcll(SH);
         }
-        const u64 DONE = __ballot(ldone);
         V3 mine = lres; /* valid where ldone */
-        for (int j = 0; j < CH; j++) {
-            const long long item = item0 + j;
-            if (item >= lp.n_items)
-                break;
-            long long slot;
-            int s;
-            item_slot(lp, item, slot, s);
-            const int pix = pixels ? pixels[slot] : (int)slot;
-            if ((DONE >> j) & 1ull)
-                continue;
+        /* the other items, one after another by the whole wave; only this mask
+         * and the lanes' (pixel, sample) stay live across the walks, not the
+         * launch fields item_slot needs */
+        for (u64 todo = __ballot(lvalid) & ~__ballot(ldone); todo; todo &= todo - 1) {
+            const int j = uni(__builtin_ctzll(todo));
             PT_T0(tt);
             const CamHit cam = {__builtin_amdgcn_readlane(ch.hit, j), rdlane(ch.t, j),
                                 (u32)__builtin_amdgcn_readlane((int)ch.ref, j), __builtin_amdgcn_readlane(ch.ex, j)};
-            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni(pix), uni(s), stk[wave], L, jump, A3l, G3l, cnt, cam);
+            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, __builtin_amdgcn_readlane(lpix, j),
+                                                 __builtin_amdgcn_readlane(ls, j), stk[wave], L, jump, A3l, G3l, cnt,
+                                                 cam);
             PT_ACC(cnt, 6, tt);
             if (lane == j)
                 mine = c;

@@ -67,6 +67,7 @@ struct SceneImpl
     std::vector<ObjRec> objects;
     int root = -1;
     int default_tex[2] = {-1, -1}; /* lazily created ColorTexture(0), ColorTexture(1) */
+    int wg_per_cu = 0;             /* resident workgroups per CU the kernel is built for (0 = auto) */
     std::map<int, std::unique_ptr<DeviceState>> devices;
     std::string last_key;
     void clear()

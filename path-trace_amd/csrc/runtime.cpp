@@ -5,12 +5,15 @@
  * constructors, flattens it into a device module (codegen.cpp), gets the
  * gfx950 code object (jit.cpp), and drives the megakernel:
  *
- *   items = (pixel slot, sample) pairs, slot-major; one wavefront per 64
- *   consecutive items (pt_render_fast / pt_render_strict); each item's
- *   radiance lands in a staging buffer; pt_reduce then sums every pixel's
- *   samples in sample order and divides by spp, exactly tracePixel's loop.
- *   Large frames run in sample passes bounded by max_buffer_bytes, the
- *   running per-pixel sums carried between passes.
+ *   items = (pixel slot, sample) pairs; a persistent grid of waves pulls
+ *   chunks of up to 32 items from a counter (pt_render_fast / _strict),
+ *   slot-major for large launches, sample-major for launches of <= 64 samples
+ *   per slot.  Reference order stages each sample's radiance and pt_reduce
+ *   sums a pixel's samples in sample order, exactly tracePixel's loop; the
+ *   group-64 order stages one pairwise partial per 32-sample block (whole
+ *   blocks per chunk) or per-sample values, and pt_reduce adds the blocks in
+ *   order.  Large frames run in sample passes bounded by max_buffer_bytes,
+ *   the running per-pixel sums carried between passes.
  *
  * This replaces RenderBlock::calcPixelColor's per-pixel tracePixel calls
  * (reference src/test.cpp:441-465); the block farm / thread pool around it
@@ -1014,6 +1017,16 @@ int pt_scene_compile(pt_scene *s, int depth)
         Generated g = generate(S(s), depth);
         code_object(g);
         S(s).last_key = g.key;
+        return PT_OK;
+    });
+}
+
+int pt_scene_set_occupancy(pt_scene *s, int workgroups_per_cu)
+{
+    return guard([&] {
+        if (workgroups_per_cu < 0 || workgroups_per_cu > 5)
+            throw Error(PT_ERR_ARG, "workgroups_per_cu must be 0 (auto) or 1..5");
+        S(s).wg_per_cu = workgroups_per_cu;
         return PT_OK;
     });
 }

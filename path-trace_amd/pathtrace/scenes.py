@@ -112,9 +112,11 @@ def scene_c2(procedural: bool = False):
     env = procedural_env(640, 480) if procedural else asset_image("test2.hdr")
     sky = Material(ColorTexture(0), ColorTexture(0),
                    MultiplyTexture((1, 1, 1), MirrorBallSkymapTexture(ImageTexture(env))))
-    # the demo's material mix (src/test.cpp:109-118) minus matBrightDiffuseWhite:
-    # its reflectance 8 makes a child's strength grow at every bounce, so the
-    # ray tree of a sample bouncing near it explodes exponentially
+    # the demo's material mix (src/test.cpp:109-118) minus matBrightDiffuseWhite
+    # (reflectance 8, |rc| = 13.9): the children of a diffuse bounce off it have
+    # strength 13.9e-4 > eps, so none of its 10^4 children is a leaf and each is
+    # a serial walk of its own; measured, the full C2 frame at 2 spp takes
+    # > 150 s on the GPU with it instead of 0.6 s
     mats = [m["diffuse"], m["mirror"], m["glass"], m["diffuse"], m["diamond"], m["mirror"], m["glass"],
             m["diffuse"]]
     objs = []
@@ -182,6 +184,13 @@ class Config:
     scene: Callable
     gpus: int = 1
     note: str = ""
+    wg_per_cu: int = 0  # pt_scene_set_occupancy (0 = as many as LDS allows)
+
+    def device_scene(self, procedural: bool = False):
+        """The config's scene as a DeviceScene, built at the config's occupancy."""
+        from . import DeviceScene
+        root = self.scene(procedural=True) if procedural else self.scene()
+        return DeviceScene(root, workgroups_per_cu=self.wg_per_cu)
 
     @property
     def screen(self):
@@ -193,6 +202,9 @@ CONFIGS: Dict[str, Config] = {
     "C2": Config("C2", 1280, 720, 256, 16, scene_c2, note="8 spheres + plane + mirror-ball env (test2.hdr)"),
     "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG"),
     "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene, tiles over 8 GPUs + RCCL reduce"),
+    # C5 at 2 workgroups per CU: its 14-primitive tree spills 1032 VGPRs at the
+    # default cap of 128 and its time is spine walks through the glass ball:
+    # 119 -> 277 Msamples/s on one MI355X
     "C5": Config("C5", 3840, 2160, 8192, 16, scene_c5, gpus=8,
-                 note="demo world + test.hdr spherical env + sky01 skybox"),
+                 note="demo world + test.hdr spherical env + sky01 skybox", wg_per_cu=2),
 }

@@ -127,5 +127,5 @@ def test_bmp_writer_format_and_tonemap(built, tmp_path):
 @pytest.mark.parametrize("name", ["C1", "C2", "C3", "C5"])
 def test_config_scenes_compile_for_gfx950(built, name):
     cfg = scenes.CONFIGS[name]
-    key = pt.DeviceScene(cfg.scene()).compile(cfg.depth)
+    key = cfg.device_scene().compile(cfg.depth)
     assert re.fullmatch(r"[0-9a-f]{16}", key)

@@ -102,7 +102,7 @@ def test_full_1080p_frame_on_sampled_pixels(built, tmp_path):
     every pixel; the oracle checks 1500 hashed pixels bit for bit."""
     cfg = scenes.CONFIGS["C3"]
     root = cfg.scene()
-    img, st = pt.render(root, cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen, stats=True)
+    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen, stats=True)
     rng = np.random.default_rng(7)
     pix = np.sort(rng.choice(cfg.width * cfg.height, 1500, replace=False)).astype(np.int32)
     o = O.render(to_text(root, str(tmp_path)), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen,
@@ -120,7 +120,7 @@ def test_benchmark_configs_on_sampled_pixels(built, tmp_path, name, spp, npix):
     the full frame on the GPU, hashed pixels bit for bit against the oracle."""
     cfg = scenes.CONFIGS[name]
     root = cfg.scene()
-    img, st = pt.render(root, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
+    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
     assert st["samples"] == cfg.width * cfg.height * spp
     rng = np.random.default_rng(11)
     pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
@@ -221,7 +221,7 @@ def test_c4_eight_shards_on_one_gpu(built, tmp_path):
     (replaces the reference's block farm, src/test.cpp:520-778)."""
     cfg = scenes.CONFIGS["C4"]
     root = cfg.scene()
-    ds = pt.DeviceScene(root)
+    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu)
     W, H, spp = cfg.width, cfg.height, 2
     full = pt.render(ds, W, H, spp, cfg.depth, screen=cfg.screen).reshape(-1, 3)
     acc = np.zeros_like(full)
@@ -281,7 +281,7 @@ def test_config_scale_vs_reference(built, name, tmp_path):
     pix, ref = z["pixels"], z["means"]
     W, H, spp, depth, seed = [int(v) for v in z["meta"][:5]]
     cfg = scenes.CONFIGS[name]
-    ds = pt.DeviceScene(cfg.scene())
+    ds = cfg.device_scene()
     g = pt.render(ds, W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix, order="reference")
     if name == "C5":
         e = rmse(g, ref)

@@ -23,7 +23,7 @@ z = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file_
                          "config_C3.npz"))
 W, H, spp, depth, seed = [int(v) for v in z["meta"][:5]]
 cfg = scenes.CONFIGS["C3"]
-ds = pt.DeviceScene(cfg.scene())
+ds = cfg.device_scene()
 for order in ["reference", "fast"]:
     print("start C3", order, flush=True)
     t = time.time()

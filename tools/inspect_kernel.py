@@ -15,7 +15,7 @@ import pathtrace as pt  # noqa: E402
 from pathtrace import scenes  # noqa: E402
 
 cfg = scenes.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "C3"]
-ds = pt.DeviceScene(cfg.scene())
+ds = cfg.device_scene()
 t = time.time()
 key = ds.compile(cfg.depth)
 print("compile %.1fs" % (time.time() - t))

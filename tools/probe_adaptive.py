@@ -12,7 +12,7 @@ from pathtrace import scenes  # noqa: E402
 
 name, spp = sys.argv[1], int(sys.argv[2])
 cfg = scenes.CONFIGS[name]
-ds = pt.DeviceScene(cfg.scene())
+ds = cfg.device_scene()
 t = time.time()
 img, info = pt.render_adaptive(ds, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen)
 ta = time.time() - t

@@ -12,7 +12,7 @@ from pathtrace import scenes  # noqa: E402
 name, W, H, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
 order = sys.argv[5] if len(sys.argv) > 5 else "fast"
 cfg = scenes.CONFIGS[name]
-ds = pt.DeviceScene(cfg.scene())
+ds = cfg.device_scene()
 screen = (float(W), float(H), float(2 * min(W, H)))
 t = time.time()
 img, st = pt.render(ds, W, H, spp, cfg.depth, screen=screen, stats=True, order=order)

@@ -21,7 +21,7 @@ name = sys.argv[1] if len(sys.argv) > 1 else "C4"
 cfg = scenes.CONFIGS[name]
 world = int(sys.argv[2]) if len(sys.argv) > 2 else cfg.gpus
 spp = int(sys.argv[3]) if len(sys.argv) > 3 else cfg.spp
-ds = pt.DeviceScene(cfg.scene())
+ds = cfg.device_scene()
 rows = []
 for r in range(world):
     pix = ptdist.rank_pixels(cfg.width, cfg.height, r, world)
