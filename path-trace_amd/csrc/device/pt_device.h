@@ -647,12 +647,18 @@ struct Sph
         const float B = dot(c.omc, w);
         const float s = (__builtin_fabsf(c.omc.x * w.x) + __builtin_fabsf(c.omc.y * w.y)) +
                         __builtin_fabsf(c.omc.z * w.z);
-        const bool pre = c.c > 0.0f && (__builtin_fabsf(c.omc.x) + __builtin_fabsf(c.omc.y)) +
-                                               __builtin_fabsf(c.omc.z) < 1e15f;
-        /* pre is wave-uniform: a scalar mask, neither a ballot of pre && x
-         * (InstCombine folds ballot(a) & ballot(b) into that) nor a branch
-         * (which would split the round's interleaved attempts) */
-        return __ballot(B > __builtin_fmaxf(1e-6f * s, 1e-30f)) & uni_mask(pre);
+        return __ballot(B > __builtin_fmaxf(1e-6f * s, 1e-30f));
+    }
+    /* The test's burst-uniform precondition, taken once per burst (the dark
+     * mask of a direction is dark_mask(w) & dark_pre: a scalar mask, neither a
+     * ballot of pre && x -- InstCombine folds ballot(a) & ballot(b) into that
+     * -- nor a branch, which would split the round's interleaved attempts) */
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_pre(const Ctx &c, const Env &)
+    {
+        if constexpr (!SEL::take(MAT))
+            return true;
+        return c.c > 0.0f && (__builtin_fabsf(c.omc.x) + __builtin_fabsf(c.omc.y)) + __builtin_fabsf(c.omc.z) < 1e15f;
     }
 };
 
@@ -759,20 +765,26 @@ struct Pln
     template <class SEL>
     __device__ static constexpr int nsel() { return SEL::take(MAT) ? 1 : 0; }
     template <class SEL>
-    __device__ static __forceinline__ u64 dark_mask(const Ctx &c, V3 w, const Env &e)
+    __device__ static __forceinline__ bool dark_pre(const Ctx &c, const Env &e)
+    {
+        if constexpr (!SEL::take(MAT))
+            return true;
+        const V3 np = mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
+        return c.num <= -(EPS * EPS) && (__builtin_fabsf(np.x) + __builtin_fabsf(np.y)) + __builtin_fabsf(np.z) <= 1.5f;
+    }
+    template <class SEL>
+    __device__ static __forceinline__ u64 dark_mask(const Ctx &, V3 w, const Env &e)
     {
         if constexpr (!SEL::take(MAT))
             return ~0ull;
         const V3 np = mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]);
-        const bool pre = c.num <= -(EPS * EPS) &&
-                         (__builtin_fabsf(np.x) + __builtin_fabsf(np.y)) + __builtin_fabsf(np.z) <= 1.5f;
         if constexpr (AX >= 0 && PT_PLANE_AXIS_DARK) {
             /* the exact n.w is n_a * w_a: its sign test is one compare (the
              * bound above holds for an exact n.w >= 0 as for a computed one) */
             const float wa = (AX >> 1) == 0 ? w.x : (AX >> 1) == 1 ? w.y : w.z;
-            return __ballot((AX & 1) ? wa <= 0.0f : wa >= 0.0f) & uni_mask(pre);
+            return __ballot((AX & 1) ? wa <= 0.0f : wa >= 0.0f);
         }
-        return __ballot(dot(w, np) >= 0.0f) & uni_mask(pre);
+        return __ballot(dot(w, np) >= 0.0f);
     }
 };
 
@@ -854,6 +866,11 @@ struct Pln
     __device__ static __forceinline__ u64 dark_mask(const Ctx &c, V3 w, const Env &e)              \
     {                                                                                               \
         return A::template dark_mask<SEL>(c.a, w, e) & B::template dark_mask<SEL>(c.b, w, e);       \
+    }                                                                                               \
+    template <class SEL>                                                                            \
+    __device__ static __forceinline__ bool dark_pre(const Ctx &c, const Env &e)                    \
+    {                                                                                               \
+        return A::template dark_pre<SEL>(c.a, e) && B::template dark_pre<SEL>(c.b, e);              \
     }
 
 /* Each merge step decides what to emit and which child to advance, then
@@ -1054,6 +1071,8 @@ struct Xf
     __device__ static constexpr int nsel() { return C::template nsel<SEL>(); }
     template <class SEL>
     __device__ static __forceinline__ u64 dark_mask(const Ctx &, V3, const Env &) { return ~0ull; }
+    template <class SEL>
+    __device__ static __forceinline__ bool dark_pre(const Ctx &, const Env &) { return true; }
 };
 
 /* First qualifying span of the root, traceRay's scan (path-trace.h:66-100). */
@@ -1698,7 +1717,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
      * dot (< 7e-5 here) cannot flip the sign.  Without RAW every child is kept
      * and the fast pass computes its exact term. */
     constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
-    const u64 raw_mask = uni_mask(KR0 || length(kR) < 64.0f);
+    /* with the dark tests' burst-uniform preconditions folded in once per
+     * burst: AND_p (ballot_p & pre_p) == (AND_p ballot_p) & AND_p pre_p */
+    const u64 raw_mask = uni_mask((KR0 || length(kR) < 64.0f) && S::Root::template dark_pre<Emissive<S>>(c0, e));
     /* queued slots hold ring numbers mod 256; every pending one lies in
      * [keep_sum, keep_sum + PT_RCAP), which restores it */
     auto slot_pos = [&](unsigned char v) { return keep_sum + ((int)(v - keep_sum) & (PT_RCAP - 1)); };
@@ -1730,13 +1751,14 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             u64 nlor = 0ull, Alast = 0ull, Flast = 0ull;
             /* one attempt's flag and (kept, with a free slot) ring entry */
             auto write_attempt = [&](bool acc, u64 A, u64 kp, V3 wn, float factor) {
-                if (acc) {
-                    const int kl = lane_bit(kp);
+                /* two flat lane-conditional stores, not nested ones (kp is a
+                 * subset of A): one exec round trip fewer per attempt */
+                const int kl = lane_bit(kp);
+                const int ko = mbcnt(kp, tk);
+                if (acc)
                     flags[mbcnt(A, npos + ta) & (PT_FCAP - 1)] = (unsigned char)kl;
-                    const int ko = mbcnt(kp, tk);
-                    if (kl && ko < free_slots)
-                        ring[(nkeep + ko) & (PT_RCAP - 1)] = make_float4(wn.x, wn.y, wn.z, factor);
-                }
+                if (kl && ko < free_slots)
+                    ring[(nkeep + ko) & (PT_RCAP - 1)] = make_float4(wn.x, wn.y, wn.z, factor);
                 ta += __popcll(A);
                 tk += __popcll(kp);
             };
