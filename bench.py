@@ -220,7 +220,8 @@ def main():
                 cfg.name, W, H, spp, cfg.depth, cfg.note,
                 ("; timed on %d hashed pixels at full spp" % subset) if subset else ""),
                        "order": args.order,
-                       "sharding": ("every pixel, spp split over ranks, per-pixel sums + RCCL reduce" if by_samples
+                       "sharding": ("one GPU renders every pixel" if world == 1 else
+                                    "every pixel, spp split over ranks, per-pixel sums + RCCL reduce" if by_samples
                                     else "16x16 tiles hashed over ranks + RCCL reduce")},
             "samples_per_step": npix_total * spp,
             "queries_per_sample": round(queries / samples, 2),

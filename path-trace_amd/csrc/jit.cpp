@@ -82,6 +82,11 @@ const char *kOptions[] = {
     "-fno-gpu-flush-denormals-to-zero",           /* keep f32 denormals as the reference does              */
     "-fno-fast-math",
     "-fno-slp-vectorize", /* packing pairs of f32 ops into v_pk_* costs more v_mov than it saves (A/B on C3) */
+    /* live-range splitting around spills sized for fewer copies: the megakernel
+     * spills at every occupancy (A/B on one box: C3 120.5 -> 124.5 Msamples/s,
+     * C2 and C5 unchanged within noise) */
+    "-mllvm",
+    "-split-spill-mode=size",
 };
 
 /* experiment hook: extra compiler options, e.g. PT_JIT_OPTIONS="-fno-slp-vectorize".

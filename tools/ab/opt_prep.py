@@ -1,7 +1,8 @@
 """Precompile the C3 megakernel for compiler-option / define variants into the
 in-tree JIT cache (no GPU) and print each variant's register use and spills.
 usage: python tools/ab/opt_prep.py "opts1" "opts2" ...   ("-" = none)
-An argument starting with "D:" is a PT_DEVICE_DEFINES variant instead."""
+An argument starting with "D:" is a PT_DEVICE_DEFINES variant instead.
+PT_PREP_CFG=C2 (etc.) compiles that benchmark config's scene instead of C3."""
 import os
 import shutil
 import subprocess
@@ -10,9 +11,11 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CACHE = os.path.join(ROOT, "path-trace_amd", "_jit_cache")
+CFG = os.environ.get("PT_PREP_CFG", "")
 code = ("import sys; sys.path.insert(0, %r)\n"
-        "import pathtrace as pt\nfrom pathtrace import scenes\n"
-        "pt.DeviceScene(scenes.scene_p1()).compile(8)\n") % os.path.join(ROOT, "path-trace_amd")
+        "import pathtrace as pt\nfrom pathtrace import scenes\n" % os.path.join(ROOT, "path-trace_amd"))
+code += ("c = scenes.CONFIGS[%r]; c.device_scene().compile(c.depth)\n" % CFG if CFG else
+         "pt.DeviceScene(scenes.scene_p1()).compile(8)\n")
 
 
 def notes(path):
