@@ -1,17 +1,22 @@
 """Per-phase wave-cycle split of the C3 render kernel (profiling build).
 Runs tools/perf_probe.py with PT_DEVICE_DEFINES=PT_PHASE_TIMING and
 PT_PHASE_DUMP=1 and prints each phase's share of the sample total.
-usage: phase_probe.py [spp] [extra defines]"""
+usage: phase_probe.py [spp] [extra defines]
+       phase_probe.py cfg CONFIG W H SPP [extra defines]   (tools/probe_cfg.py instead)"""
 import os
 import subprocess
 import sys
 
 here = os.path.dirname(os.path.abspath(__file__))
-spp = sys.argv[1] if len(sys.argv) > 1 else "16"
-defs = " ".join(["PT_PHASE_TIMING"] + sys.argv[2:])
+if len(sys.argv) > 1 and sys.argv[1] == "cfg":
+    cmd = [sys.executable, os.path.join(here, "probe_cfg.py")] + sys.argv[2:6]
+    extra = sys.argv[6:]
+else:
+    cmd = [sys.executable, os.path.join(here, "perf_probe.py"), sys.argv[1] if len(sys.argv) > 1 else "16"]
+    extra = sys.argv[2:]
+defs = " ".join(["PT_PHASE_TIMING"] + extra)
 env = dict(os.environ, PT_DEVICE_DEFINES=defs, PT_PHASE_DUMP="1")
-r = subprocess.run([sys.executable, os.path.join(here, "perf_probe.py"), spp], env=env, capture_output=True,
-                   text=True, timeout=900)
+r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
 print(r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "no stdout", r.stderr[-1500:] if r.returncode else "")
 names = ["generation", "gen-attempts", "fastpass", "slowpass", "groupsum", "burst", "sample"]
 for line in r.stderr.splitlines():
