@@ -522,6 +522,7 @@ template <int PRIM, int OFF, int MAT>
 struct Sph
 {
     static constexpr int LO = PRIM, HI = PRIM + 1;
+    static constexpr bool UNION_ONLY = true; /* no Intersection / Difference at or below */
     struct Ctx
     {
         V3 omc;
@@ -672,6 +673,7 @@ template <int PRIM, int OFF, int MAT, int AX = -1>
 struct Pln
 {
     static constexpr int LO = PRIM, HI = PRIM + 1;
+    static constexpr bool UNION_ONLY = true; /* no Intersection / Difference at or below */
     struct Ctx
     {
         float num;
@@ -882,6 +884,7 @@ template <class A, class B>
 struct Uni
 {
     static constexpr int KIND = NODE_UNION;
+    static constexpr bool UNION_ONLY = A::UNION_ONLY && B::UNION_ONLY;
     PTD_BINARY_COMMON
     template <class SEL>
     __device__ static constexpr bool clear_ok() { return A::template clear_ok<SEL>() && B::template clear_ok<SEL>(); }
@@ -929,6 +932,7 @@ template <class A, class B>
 struct Isect
 {
     static constexpr int KIND = NODE_ISECT;
+    static constexpr bool UNION_ONLY = false;
     PTD_BINARY_COMMON
     template <class SEL>
     __device__ static constexpr bool clear_ok() { return A::template nsel<SEL>() + B::template nsel<SEL>() == 0; }
@@ -972,6 +976,7 @@ template <class A, class B>
 struct Diff
 {
     static constexpr int KIND = NODE_DIFF;
+    static constexpr bool UNION_ONLY = false;
     PTD_BINARY_COMMON
     template <class SEL>
     __device__ static constexpr bool clear_ok() { return A::template nsel<SEL>() + B::template nsel<SEL>() == 0; }
@@ -1022,6 +1027,7 @@ template <int MOFF, int IOFF, class C>
 struct Xf
 {
     static constexpr int LO = C::LO, HI = C::HI;
+    static constexpr bool UNION_ONLY = C::UNION_ONLY; /* spans keep the ray's t */
     struct Ctx
     {
         typename C::Ctx c;
@@ -1128,6 +1134,35 @@ __device__ __forceinline__ bool fast_first_hit(const PS &ps, float &t, int &mat)
     return true;
 }
 
+/* Union merges (src/union.cpp:84-134) turn the spans below a node into the
+ * connected components of their union (overlapping or touching spans merge,
+ * the smaller start kept).  So where only Unions (and transforms, which keep
+ * the ray's t) combine a set of primitives, and b0 -- the smallest start among
+ * their live spans reaching EPS -- is itself >= EPS and no other such span
+ * starts at b0, the first component reaching EPS starts at b0: a span ending
+ * before EPS cannot touch it and every other span reaching EPS starts later.
+ * traceRay's scan (path-trace.h:66-100) stops there, at fast_first_hit's /
+ * sel_first_hit's answer, however the spans overlap: one pass over the spans
+ * instead of the pairwise separation checks.  No candidate at all: nothing is
+ * hit.  NaN bounds never pass. */
+template <class PS, class EACH>
+__device__ __forceinline__ int union_min_ok(const PS &ps, EACH &&each)
+{
+    int found = 0, tie = 0, bad = 0;
+    float b0 = 0.0f;
+    each([&](auto x, auto) {
+        constexpr int X = decltype(x)::value;
+        const int live = ps.live[X];
+        const int cand = live & (ps.t1[X] >= EPS);
+        const int better = cand & ((!found) | (ps.t0[X] < b0));
+        tie = better ? 0 : (tie | (cand & (ps.t0[X] == b0)));
+        bad |= live & ((ps.t0[X] != ps.t0[X]) | (ps.t1[X] != ps.t1[X]));
+        b0 = better ? ps.t0[X] : b0;
+        found |= cand;
+    });
+    return ((!found) | ((b0 >= EPS) & !tie)) & !bad;
+}
+
 /* ---- clear pass -------------------------------------
  * When every selected (emissive) primitive is reached from the root through
  * Union and TransformedObject nodes only (R::clear_ok), and on a lane every
@@ -1144,6 +1179,26 @@ __device__ __forceinline__ bool fast_first_hit(const PS &ps, float &t, int &mat)
  * former and stops at that same end in the latter.  So the first hit is
  * fast_first_hit over the selected primitives alone, checked pairwise like
  * the fast pass (pair_ok at a Union) when there are several. */
+template <class R, class SEL, class PS>
+__device__ __forceinline__ int sel_pairs_ok(const PS &ps);
+/* The clear pass's check over the selected primitives: with two or more, the
+ * union rule above first (they hang off the root through Unions and
+ * transforms only, and every other span ends before EPS), the pairwise checks
+ * only on the lanes it cannot decide. */
+template <class R, class SEL, class PS>
+__device__ __forceinline__ int sel_ok(const PS &ps)
+{
+    if constexpr (R::template nsel<SEL>() < 2) {
+        return sel_pairs_ok<R, SEL>(ps);
+    } else {
+        int ok = union_min_ok(ps, [&](auto &&f) { R::template each_sel<SEL>(f); });
+        if (wave_any(!ok)) {
+            if (!ok)
+                ok = sel_pairs_ok<R, SEL>(ps);
+        }
+        return ok;
+    }
+}
 template <class R, class SEL, class PS>
 __device__ __forceinline__ int sel_pairs_ok(const PS &ps)
 {
@@ -1915,7 +1970,18 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             PT_MARK(9);
             S::Root::span(ps, ctx, mkray(dir), e);
             PT_MARK(10);
-            const int fok = S::Root::fast_ok(ps);
+            int fok;
+            if constexpr (S::Root::UNION_ONLY) {
+                /* the union rule over every primitive; the pairwise checks
+                 * only where it cannot decide */
+                fok = union_min_ok(ps, [&](auto &&f) { S::Root::each_pos(f); });
+                if (wave_any(!fok)) {
+                    if (!fok)
+                        fok = S::Root::fast_ok(ps);
+                }
+            } else {
+                fok = S::Root::fast_ok(ps);
+            }
             PT_MARK(11);
             if (fok) {
                 float t = 0.0f;
@@ -2032,7 +2098,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                             const u64 CM = S::Root::template clear_mask<Emissive<S>, true>(ctx, q, e);
                             PrimSpans<S::Root::HI> ps;
                             S::Root::template span_sel<Emissive<S>>(ps, ctx, q, e);
-                            if (((CM >> lane) & 1ull) && sel_pairs_ok<typename S::Root, Emissive<S>>(ps)) {
+                            if (((CM >> lane) & 1ull) && sel_ok<typename S::Root, Emissive<S>>(ps)) {
                                 float t = 0.0f;
                                 int mat = 0;
                                 V3 col = mk(0, 0, 0);
