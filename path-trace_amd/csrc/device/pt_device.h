@@ -1764,7 +1764,10 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     int fast_on = 1, clear_on = 1;
     /* the clear pass applies when every emissive primitive hangs off the root
      * through Unions and transforms only */
-    constexpr bool CLEAR = S::Root::template clear_ok<Emissive<S>>();
+    /* union-only scenes skip it: their first pass takes every primitive's
+     * span and the union rule at once, which decides nearly every lane and
+     * saves the mid queue's second pass (C2 2.94 -> 3.37 Msamples/s) */
+    constexpr bool CLEAR = S::Root::template clear_ok<Emissive<S>>() && !S::Root::UNION_ONLY;
     /* RAW: dark children are decided on the unnormalised direction (dark_mask,
      * sound but conservative).  The Z shortcut also needs a factor >= +0, i.e.
      * a computed dot(normalize(w), n) >= 0: accepted w have a computed
