@@ -182,8 +182,10 @@ typedef struct pt_adaptive_params {
     int block_size;
     int max_interp;
     float min_delta;
-    int64_t traced_pixels;         /* out: pixels traced                                       */
+    int64_t traced_pixels;         /* out: pixels traced whose colour the image used            */
     int levels;                    /* out: GPU batches                                          */
+    int exact_batches;             /* in: nonzero = one batch per level, only needed points     */
+    int64_t lookahead_pixels;      /* out: traced one level ahead and never used                */
 } pt_adaptive_params;
 int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_params *ap, float *rgb_out,
                        pt_render_stats *stats);

@@ -1177,17 +1177,30 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
                          std::vector<char>((size_t)(S + 1) * (S + 1), 0)};
                 blocks.push_back(std::move(b));
             }
-        std::map<int64_t, AV> traced;
+        struct TP
+        {
+            AV c;
+            bool used;
+        };
+        std::map<int64_t, TP> traced;
         std::vector<int32_t> need;
+        /* Lookahead: a batch that runs anyway also traces the next level's
+         * possible points (the five midpoints of every square the next level
+         * could split), so the level after it usually needs no batch of its
+         * own -- half the launches, each of which waits on its slowest sample.
+         * A point's colour depends only on its (x, y) and the sample indices,
+         * never on the batch, so the image is the same bits either way. */
+        const bool lookahead = ap->exact_batches == 0;
         pt_render_stats acc;
         memset(&acc, 0, sizeof acc);
         ap->traced_pixels = 0;
+        ap->lookahead_pixels = 0;
         ap->levels = 0;
         auto want = [&](int x, int y) {
             const int64_t k = (int64_t)y * gw + x;
             if (k < 0 || k > INT32_MAX)
                 throw Error(PT_ERR_ARG, "adaptive block reaches past the index range");
-            if (traced.emplace(k, AV{0, 0, 0}).second)
+            if (traced.emplace(k, TP{AV{0, 0, 0}, false}).second)
                 need.push_back((int32_t)k);
         };
         auto flush = [&]() {
@@ -1202,12 +1215,12 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
             int rc = pt_render(s, &q, out.data(), &st);
             if (rc != PT_OK)
                 throw Error(rc, pt_last_error());
-            for (size_t k = 0; k < need.size(); k++) traced[need[k]] = AV{out[3 * k], out[3 * k + 1], out[3 * k + 2]};
+            for (size_t k = 0; k < need.size(); k++)
+                traced[need[k]].c = AV{out[3 * k], out[3 * k + 1], out[3 * k + 2]};
             acc.kernel_ms += st.kernel_ms, acc.reduce_ms += st.reduce_ms, acc.launches += st.launches;
             acc.samples += st.samples, acc.queries += st.queries, acc.leaf_queries += st.leaf_queries;
             acc.attempts += st.attempts, acc.rounds += st.rounds, acc.slow_queries += st.slow_queries;
             acc.dark_queries += st.dark_queries;
-            ap->traced_pixels += (int64_t)need.size();
             ap->levels++;
             need.clear();
         };
@@ -1215,13 +1228,31 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
         auto calc = [&](ABlock &b, int x, int y) {
             if (b.traced(x, y))
                 return b.buf[b.at(x, y)];
-            AV c = traced.at((int64_t)y * gw + x);
-            b.set_traced(x, y, c);
-            return c;
+            TP &t = traced.at((int64_t)y * gw + x);
+            t.used = true;
+            b.set_traced(x, y, t.c);
+            return t.c;
+        };
+        /* the five points a square's split traces (renderSquare, :478-491) */
+        auto mids = [&](int x, int y, int size, const ABlock &b) {
+            const int h = size / 2, cx = x + h, cy = y + h;
+            const int pts[5][2] = {{cx, y}, {x, cy}, {cx, cy}, {x + size, cy}, {cx, y + size}};
+            for (const auto &pt : pts)
+                if (!b.traced(pt[0], pt[1]))
+                    want(pt[0], pt[1]);
+        };
+        /* the next level's possible points: the midpoints of every square of
+         * size `size` at (x, y) that level could split */
+        auto ahead = [&](int x, int y, int size, const ABlock &b) {
+            if (!lookahead || size <= 1 || x > W || y > H)
+                return;
+            mids(x, y, size, b);
         };
         for (ABlock &b : blocks) {
             want(b.x0, b.y0), want(b.x0 + S, b.y0), want(b.x0, b.y0 + S), want(b.x0 + S, b.y0 + S);
         }
+        for (ABlock &b : blocks)
+            ahead(b.x0, b.y0, S, b);
         flush();
         std::vector<ASquare> cur;
         for (size_t i = 0; i < blocks.size(); i++) { /* RenderBlock::run, :501-507 */
@@ -1255,14 +1286,16 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
                     }
                     continue;
                 }
-                const int h = q.size / 2, cx = q.x + h, cy = q.y + h;
-                auto maybe = [&](int x, int y) {
-                    if (!b.traced(x, y))
-                        want(x, y);
-                };
-                maybe(cx, q.y), maybe(q.x, cy), maybe(cx, cy), maybe(q.x + q.size, cy), maybe(cx, q.y + q.size);
+                mids(q.x, q.y, q.size, b);
                 split.push_back(q);
             }
+            /* a batch runs for this level: add the next level's possible points */
+            if (!need.empty())
+                for (const ASquare &q : split) {
+                    const int h = q.size / 2, cx = q.x + h, cy = q.y + h;
+                    const ABlock &b = blocks[q.b];
+                    ahead(q.x, q.y, h, b), ahead(cx, q.y, h, b), ahead(q.x, cy, h, b), ahead(cx, cy, h, b);
+                }
             flush();
             std::vector<ASquare> next;
             for (const ASquare &q : split) {
@@ -1277,6 +1310,8 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
             }
             cur.swap(next);
         }
+        for (const auto &kv : traced)
+            (kv.second.used ? ap->traced_pixels : ap->lookahead_pixels)++;
         /* copyToBuffer, :362-374: each block's interior, valid pixels only */
         std::fill(rgb_out, rgb_out + (size_t)W * H * 3, 0.0f);
         for (const ABlock &b : blocks)

@@ -165,21 +165,26 @@ def render(scene, width: int, height: int, spp: int, depth: int, screen=None, se
 
 
 def render_adaptive(scene, width: int, height: int, spp: int, depth: int, screen=None, seed: int = 0x5EED,
-                    order="fast", block_size: int = 0, max_interp: int = 0, min_delta: float = 0.0, device: int = 0):
+                    order="fast", block_size: int = 0, max_interp: int = 0, min_delta: float = 0.0, device: int = 0,
+                    exact_batches: bool = False):
     """The reference demo's adaptive image formation (RenderBlock::renderSquare,
     src/test.cpp:423-507) on the GPU: returns (H x W x 3 image, info dict with
-    traced_pixels, levels and the render stats).  0 selects the demo's block
-    size / interpolation limit / colour threshold."""
+    traced_pixels (used), lookahead_pixels (traced ahead, unused), levels (GPU
+    batches) and the render stats).  0 selects the demo's block size /
+    interpolation limit / colour threshold.  exact_batches: one batch per
+    level with only the needed points (the image is the same bits)."""
     ds = scene if isinstance(scene, DeviceScene) else DeviceScene(scene)
     p, _ = make_params(width, height, spp, depth, screen, seed, order, device)
     ap = _lib.AdaptiveParams()
     ap.block_size, ap.max_interp, ap.min_delta = int(block_size), int(max_interp), float(min_delta)
+    ap.exact_batches = 1 if exact_batches else 0
     out = np.zeros((height, width, 3), dtype=np.float32)
     st = RenderStats()
     _lib.check(_lib.lib().pt_render_adaptive(ds.handle, ctypes.byref(p), ctypes.byref(ap), out.ctypes.data,
                                              ctypes.byref(st)))
     info = st.as_dict()
-    info.update(traced_pixels=int(ap.traced_pixels), levels=int(ap.levels))
+    info.update(traced_pixels=int(ap.traced_pixels), levels=int(ap.levels),
+                lookahead_pixels=int(ap.lookahead_pixels))
     return out, info
 
 

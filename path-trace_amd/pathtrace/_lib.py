@@ -32,7 +32,8 @@ class RenderParams(ctypes.Structure):
 
 class AdaptiveParams(ctypes.Structure):
     _fields_ = [("block_size", ctypes.c_int), ("max_interp", ctypes.c_int), ("min_delta", ctypes.c_float),
-                ("traced_pixels", ctypes.c_int64), ("levels", ctypes.c_int)]
+                ("traced_pixels", ctypes.c_int64), ("levels", ctypes.c_int), ("exact_batches", ctypes.c_int),
+                ("lookahead_pixels", ctypes.c_int64)]
 
 
 class RenderStats(ctypes.Structure):

@@ -128,3 +128,10 @@ def test_gpu_adaptive_matches_oracle(built, tmp_path, builder, W, H, spp, depth,
     assert diff.size == 0, "%d mismatches, first %s" % (diff.size, diff[:4])
     # the GPU traces each distinct pixel once; the oracle once per block that needs it
     assert 0 < info["traced_pixels"] <= traced
+    # lookahead batching (the default) and one batch per level: the same bits,
+    # the same used points, fewer batches
+    img2, info2 = pt.render_adaptive(root, W, H, spp, depth, block_size=block, max_interp=max_interp,
+                                     min_delta=delta, exact_batches=True)
+    np.testing.assert_array_equal(img2.view(np.uint32), img.view(np.uint32))
+    assert info2["traced_pixels"] == info["traced_pixels"] and info2["lookahead_pixels"] == 0
+    assert info["levels"] <= info2["levels"]

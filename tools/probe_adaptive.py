@@ -14,13 +14,19 @@ name, spp = sys.argv[1], int(sys.argv[2])
 cfg = scenes.CONFIGS[name]
 ds = cfg.device_scene()
 t = time.time()
+img_x, info_x = pt.render_adaptive(ds, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, exact_batches=True)
+tx = time.time() - t
+t = time.time()
 img, info = pt.render_adaptive(ds, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen)
 ta = time.time() - t
+assert (img.view(np.uint32) == img_x.view(np.uint32)).all()
 t = time.time()
 full, st = pt.render(ds, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
 tf = time.time() - t
 rmse = np.sqrt(np.mean((img.astype(np.float64) - full) ** 2, axis=(0, 1))).tolist()
 print(json.dumps({"config": name, "spp": spp, "adaptive_wall_s": ta, "adaptive_kernel_ms": info["kernel_ms"],
                   "traced_pixels": info["traced_pixels"], "traced_frac": info["traced_pixels"] / (cfg.width * cfg.height),
-                  "levels": info["levels"], "full_wall_s": tf, "full_kernel_ms": st["kernel_ms"],
+                  "levels": info["levels"], "lookahead_pixels": info["lookahead_pixels"],
+                  "exact_batches": {"wall_s": tx, "kernel_ms": info_x["kernel_ms"], "levels": info_x["levels"]},
+                  "full_wall_s": tf, "full_kernel_ms": st["kernel_ms"],
                   "rmse_adaptive_vs_full": rmse}), flush=True)
