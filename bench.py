@@ -240,8 +240,12 @@ def main():
                 out["roofline"].update({
                     "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE, %s)" %
                                     os.path.relpath(PMC_JSON % cfg.name, ROOT),
-                    "valu_busy": round(ev["valu_busy"], 4), "salu_busy": round(ev["salu_busy"], 4),
+                    # issue rate against the wave64 VALU ceiling of one instruction per 2 SIMD-cycles
+                    # (rocprof's VALUBusy sums in-flight cycles over waves and exceeds 1 here)
                     "valu_insts_per_simd_cycle": round(ev.get("valu_insts_per_simd_cycle", 0), 4),
+                    "valu_issue_frac": round(ev.get("valu_insts_per_simd_cycle", 0) / 0.5, 4),
+                    "salu_insts_per_simd_cycle": round(ev.get("salu_insts_per_simd_cycle", 0), 4),
+                    "valu_busy_rocprof": round(ev["valu_busy"], 4),
                     "hbm_GBps": round(ev["hbm_GBps"], 2), "hbm_peak_GBps": 8000.0})
         if not args.no_cpu and world == 1:
             try:

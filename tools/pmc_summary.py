@@ -44,8 +44,9 @@ gui = busy["GRBM_GUI_ACTIVE"] / XCDS
 res = {
     "kernel": "pt_render_fast", "workload": b["config"]["workload"], "bench_value": b["value"],
     "valu_busy": busy["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / gui,
-    # > 1 on gfx950: more than one VALU instruction is active per quad-cycle
-    # per SIMD (co-issue), so also report the issue rate itself
+    # > 1 here: SQ_ACTIVE_INST_VALU is summed over waves, and several waves'
+    # VALU instructions are in flight on one SIMD at once, so also report the
+    # issue rate itself (ceiling 0.5 per SIMD-cycle for wave64)
     "valu_insts_per_simd_cycle": busy["SQ_INSTS_VALU"] / SIMDS / gui,
     "salu_insts_per_simd_cycle": busy["SQ_INSTS_SALU"] / SIMDS / gui,
     "salu_busy": busy["SQ_ACTIVE_INST_SCA"] * 4 / SIMDS / gui,
