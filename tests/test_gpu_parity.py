@@ -97,6 +97,19 @@ def test_fast_order_bitexact_vs_oracle_and_within_bar(built, tmp_path, case):
     assert np.all(e <= RMSE_BAR) and np.all(e <= 1e-5), e
 
 
+@pytest.mark.parametrize("order", ["fast", "reference"])
+def test_union_rule_overlaps_and_ties_bitexact(built, tmp_path, order):
+    """Union-only scene with overlapping, nested and exactly coincident spans
+    (equal starts: the union rule must defer to the pairwise checks / the full
+    merge): bit-identical to the oracle in both summation orders."""
+    root = T.union_zoo()
+    W, H, spp, depth = 48, 32, 4, 6
+    g = pt.render(root, W, H, spp, depth, order=order)
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth,
+                 order=O.ORDER_GROUP64 if order == "fast" else O.ORDER_REFERENCE)
+    assert_bits(g, o, "union zoo, %s order vs oracle" % order)
+
+
 def test_full_1080p_frame_on_sampled_pixels(built, tmp_path):
     """BASELINE's full frame size (C3 scene, 1920x1080) at 2 spp: the GPU renders
     every pixel; the oracle checks 1500 hashed pixels bit for bit."""

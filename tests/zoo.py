@@ -112,6 +112,8 @@ RENDER_CASES = [
     ("texm", "texture_transc_zoo", 32, 24, 3, 5),
 ]
 EXACT_CASES = [c for c in RENDER_CASES if c[0] != "texm"]
+# (builder, depth) of scenes only the GPU tests render (against the oracle, no goldens)
+GPU_ONLY_CASES = [("union_zoo", 6)]
 
 
 def build(name):
@@ -119,3 +121,25 @@ def build(name):
     if hasattr(scenes, name):
         return getattr(scenes, name)()
     return globals()[name]()
+
+
+def union_zoo():
+    """Union-only scene for the union rule (pt_device.h union_min_ok): an
+    emissive box of six inward half-spaces, spheres that overlap, nest and
+    coincide exactly (equal spans: ties the rule must hand to the pairwise
+    checks), a ground plane with an exact duplicate, and an emissive sphere
+    inside a glass one."""
+    diffuse = Material(ColorTexture(0.8, 0.7, 0.6), ColorTexture(1))
+    glossy = Material(ColorTexture(0.9), ColorTexture(0.3))
+    glass = Material(ColorTexture(0.7), ColorTexture(0), ColorTexture(0), ColorTexture(0.9, 0.95, 1.0), 1.45,
+                     ColorTexture(0.8))
+    mirror = Material(ColorTexture(0.99), ColorTexture(0))
+    emit = Material(ColorTexture(0), ColorTexture(0), ColorTexture(1.5, 1.2, 0.9))
+    sky = Material(ColorTexture(0), ColorTexture(0), ColorTexture(0.4, 0.6, 1.0))
+    objs = [Sphere((-1.0, 0.0, -4.0), 0.6, diffuse), Sphere((-0.4, 0.1, -4.1), 0.6, glossy),  # overlapping
+            Sphere((1.0, 0.0, -4.0), 0.6, mirror), Sphere((1.0, 0.0, -4.0), 0.6, diffuse),     # coincident
+            Sphere((0.0, 0.9, -4.5), 0.7, glass), Sphere((0.0, 0.9, -4.5), 0.25, emit),       # nested
+            Plane((0, 1, 0), 0.7, diffuse), Plane((0, 1, 0), 0.7, glossy)]                    # duplicate ground
+    for n in [(0, 0, -1), (0, 0, 1), (0, -1, 0), (0, 1, 0), (1, 0, 0), (-1, 0, 0)]:
+        objs.append(Plane(n, 60, sky))
+    return union_array(objs)
