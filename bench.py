@@ -156,7 +156,7 @@ def main():
     spp = args.spp or cfg.spp
     W, H = cfg.width, cfg.height
     root = cfg.scene()
-    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu)
+    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine)
     subset = SUBSET.get(cfg.name, 0) if args.subset < 0 else args.subset
     by_samples = world > 1 and args.split == "samples"
     mine = ptdist.rank_pixels(W, H, rank, 1 if by_samples else world)

@@ -240,6 +240,9 @@ Generated generate(const SceneImpl &s, int depth)
     /* per-scene occupancy (pt_scene_set_occupancy): the launch bounds' workgroups per CU */
     if (s.wg_per_cu > 0)
         src << "#define PT_MIN_WAVES " << s.wg_per_cu << "\n";
+    /* per-scene spine query form (pt_scene_set_fast_spine) */
+    if (s.fast_spine)
+        src << "#define PT_FAST_SPINE 1\n";
     /* experiment hook: A/B a different device library text in the same run,
      * e.g. PT_DEVICE_HEADER=tools/ab/old.h (profiling only) */
     if (const char *hdr = getenv("PT_DEVICE_HEADER")) {

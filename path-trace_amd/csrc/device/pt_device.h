@@ -1106,6 +1106,50 @@ __device__ __forceinline__ bool first_hit(const typename R::Ctx &ctx, V3 d, cons
     return false;
 }
 
+/* The spine's query (one ray, the same on every lane): every primitive's span
+ * at once and the fast checks; where they hold, the first hit is a positive
+ * primitive's own boundary -- its start (entry) if that is >= EPS, else its
+ * end (exit, the pairs around it strictly separated), never a flipped one --
+ * so the reference's ref and exit flag follow from the chosen primitive.
+ * Otherwise the lazy merge, as before.  The checks are wave-uniform here. */
+template <class R>
+__device__ __forceinline__ bool spine_first_hit(const typename R::Ctx &ctx, V3 d, const Env &e, float &t, u32 &ref,
+                                                bool &exit_hit)
+{
+    PrimSpans<R::HI> ps;
+    R::span(ps, ctx, mkray(d), e);
+    int fok;
+    if constexpr (R::UNION_ONLY)
+        fok = union_min_ok(ps, [&](auto &&f) { R::each_pos(f); }) || R::fast_ok(ps);
+    else
+        fok = R::fast_ok(ps);
+    if (!wave_any(!fok)) {
+        int found = 0;
+        u32 bref = 0u;
+        float b0 = 0.0f, b1 = 0.0f;
+        R::each_pos([&](auto x, auto m) {
+            constexpr int X = decltype(x)::value;
+            const int cand = ps.live[X] & (ps.t1[X] >= EPS);
+            const int better = cand & ((!found) | (ps.t0[X] < b0));
+            b0 = better ? ps.t0[X] : b0;
+            b1 = better ? ps.t1[X] : b1;
+            bref = better ? mkref(X, decltype(m)::value, 0) : bref;
+            found |= cand;
+        });
+        if (!found || b0 >= MAXV)
+            return false;
+        if (b0 >= EPS) {
+            t = b0, ref = bref, exit_hit = false;
+            return true;
+        }
+        if (b1 >= MAXV)
+            return false;
+        t = b1, ref = bref | 2u, exit_hit = true; /* mkref(prim, mat, 1) */
+        return true;
+    }
+    return first_hit<R>(ctx, d, e, t, ref, exit_hit);
+}
+
 /* Fast first hit over precomputed primitive spans; valid when R::fast_ok. */
 template <class R, class PS>
 __device__ __forceinline__ bool fast_first_hit(const PS &ps, float &t, int &mat)
@@ -2361,7 +2405,11 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
 #endif
                 typename S::Root::Ctx ctx;
                 S::Root::prep(ctx, o, e);
+#ifdef PT_FAST_SPINE /* per scene, pt_scene_set_fast_spine */
+                found = spine_first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+#else
                 found = first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+#endif
 #ifdef PT_SPINE_TIMING
                 PT_ACC(cnt, 0, tq);
 #endif

@@ -1032,6 +1032,14 @@ int pt_scene_set_occupancy(pt_scene *s, int workgroups_per_cu)
     });
 }
 
+int pt_scene_set_fast_spine(pt_scene *s, int on)
+{
+    return guard([&] {
+        S(s).fast_spine = on ? 1 : 0;
+        return PT_OK;
+    });
+}
+
 const char *pt_scene_kernel_key(pt_scene *s, int depth)
 {
     thread_local std::string k;

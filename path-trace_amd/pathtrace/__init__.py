@@ -36,13 +36,15 @@ class DeviceScene:
     """A pt_scene built from a Python scene graph through the C-ABI
     constructors (one pt_* call per reference constructor)."""
 
-    def __init__(self, root: Object, workgroups_per_cu: int = 0):
+    def __init__(self, root: Object, workgroups_per_cu: int = 0, fast_spine: bool = False):
         L = _lib.lib()
         self._h = L.pt_scene_create()
         if not self._h:
             raise PtError("pt_scene_create failed")
         if workgroups_per_cu:
             _lib.check(L.pt_scene_set_occupancy(self._h, int(workgroups_per_cu)))
+        if fast_spine:
+            _lib.check(L.pt_scene_set_fast_spine(self._h, 1))
         self._img = {}
         self._mat = {}
         self.root = root

@@ -93,6 +93,7 @@ SIGNATURES = {
     "pt_prepare": (_I, [_P, ctypes.POINTER(RenderParams)]),
     "pt_scene_compile": (_I, [_P, _I]),
     "pt_scene_set_occupancy": (_I, [_P, _I]),
+    "pt_scene_set_fast_spine": (_I, [_P, _I]),
     "pt_scene_kernel_key": (ctypes.c_char_p, [_P, _I]),
     "pt_selftest_math": (_I, [_I, ctypes.c_uint64, ctypes.c_uint64, _P]),
     "pt_write_hdr": (_I, [ctypes.c_char_p, _P, _I, _I]),

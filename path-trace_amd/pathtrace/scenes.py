@@ -185,12 +185,13 @@ class Config:
     gpus: int = 1
     note: str = ""
     wg_per_cu: int = 0  # pt_scene_set_occupancy (0 = as many as LDS allows)
+    fast_spine: bool = False  # pt_scene_set_fast_spine
 
     def device_scene(self, procedural: bool = False):
         """The config's scene as a DeviceScene, built at the config's occupancy."""
         from . import DeviceScene
         root = self.scene(procedural=True) if procedural else self.scene()
-        return DeviceScene(root, workgroups_per_cu=self.wg_per_cu)
+        return DeviceScene(root, workgroups_per_cu=self.wg_per_cu, fast_spine=self.fast_spine)
 
     @property
     def screen(self):
@@ -206,5 +207,5 @@ CONFIGS: Dict[str, Config] = {
     # default cap of 128 and its time is spine walks through the glass ball:
     # 119 -> 277 Msamples/s on one MI355X
     "C5": Config("C5", 3840, 2160, 8192, 16, scene_c5, gpus=8,
-                 note="demo world + test.hdr spherical env + sky01 skybox", wg_per_cu=2),
+                 note="demo world + test.hdr spherical env + sky01 skybox", wg_per_cu=2, fast_spine=True),
 }

@@ -110,12 +110,24 @@ def test_union_rule_overlaps_and_ties_bitexact(built, tmp_path, order):
     assert_bits(g, o, "union zoo, %s order vs oracle" % order)
 
 
+@pytest.mark.parametrize("builder,depth", [("csg_zoo", 6), ("scene_p1", 8), ("union_zoo", 6)])
+def test_fast_spine_bitexact(built, tmp_path, builder, depth):
+    """pt_scene_set_fast_spine: wave-walked queries take every span and the
+    fast checks first (lazy merge only where they cannot decide): the same
+    bits as the oracle on CSG with Difference/Intersection/transforms."""
+    root = T.build(builder)
+    W, H, spp = 40, 24, 3
+    g = pt.render(pt.DeviceScene(root, fast_spine=True), W, H, spp, depth, order="fast")
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_GROUP64)
+    assert_bits(g, o, "fast spine, %s vs oracle" % builder)
+
+
 def test_full_1080p_frame_on_sampled_pixels(built, tmp_path):
     """BASELINE's full frame size (C3 scene, 1920x1080) at 2 spp: the GPU renders
     every pixel; the oracle checks 1500 hashed pixels bit for bit."""
     cfg = scenes.CONFIGS["C3"]
     root = cfg.scene()
-    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen, stats=True)
+    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen, stats=True)
     rng = np.random.default_rng(7)
     pix = np.sort(rng.choice(cfg.width * cfg.height, 1500, replace=False)).astype(np.int32)
     o = O.render(to_text(root, str(tmp_path)), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen,
@@ -128,12 +140,12 @@ def test_full_1080p_frame_on_sampled_pixels(built, tmp_path):
 @pytest.mark.parametrize("name,spp,npix", [("C1", 4, 2000), ("C2", 2, 300), ("C5", 2, 2000)])
 def test_benchmark_configs_on_sampled_pixels(built, tmp_path, name, spp, npix):
     """The other benchmark workloads: C1 (P0), C2 (mirror-ball
-    env, depth 16, half-space sky box -- every leaf takes the full merge) and
+    env, depth 16, overlapping half-space sky box: the union rule) and
     C5 (demo world, lens = Intersection, TransformedTexture, skybox, 4K):
     the full frame on the GPU, hashed pixels bit for bit against the oracle."""
     cfg = scenes.CONFIGS[name]
     root = cfg.scene()
-    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
+    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
     assert st["samples"] == cfg.width * cfg.height * spp
     rng = np.random.default_rng(11)
     pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
@@ -234,7 +246,7 @@ def test_c4_eight_shards_on_one_gpu(built, tmp_path):
     (replaces the reference's block farm, src/test.cpp:520-778)."""
     cfg = scenes.CONFIGS["C4"]
     root = cfg.scene()
-    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu)
+    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine)
     W, H, spp = cfg.width, cfg.height, 2
     full = pt.render(ds, W, H, spp, cfg.depth, screen=cfg.screen).reshape(-1, 3)
     acc = np.zeros_like(full)
