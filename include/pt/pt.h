@@ -206,12 +206,13 @@ int pt_scene_compile(pt_scene *s, int depth);
  * samples are mostly spine walks run faster (C5: 2.3x at 2), burst-bound
  * scenes slower (C2 at 2: -8 %).  Takes effect at the next compile/render. */
 int pt_scene_set_occupancy(pt_scene *s, int workgroups_per_cu);
-/* MI355X tuning knob, no reference counterpart: the wave-walked (spine)
- * queries of this scene first take every primitive's span and the fast
- * checks, and run the lazy merge only where those cannot decide (same bits
- * either way).  Pays where spine rays rarely start inside overlapping CSG
- * spans (C5's glass-ball walks: 288 -> 421 Msamples/s), costs where they
- * often do (C3: -0.9 %).  Takes effect at the next compile/render. */
+/* MI355X tuning knob, no reference counterpart: the wave-walked (spine) and
+ * lane-walked (camera, lane-finished child) queries of this scene first take
+ * every primitive's span and the fast checks, and run the lazy merge only
+ * where those cannot decide (same bits either way).  Pays where rays rarely
+ * start inside overlapping CSG spans (C5: 288 -> 568 Msamples/s), costs
+ * where they often do (C3 spine: -0.9 %).  Takes effect at the next
+ * compile/render. */
 int pt_scene_set_fast_spine(pt_scene *s, int on);
 /* Key of the code object for this scene/depth (hex string, static storage). */
 const char *pt_scene_kernel_key(pt_scene *s, int depth);

@@ -1106,48 +1106,77 @@ __device__ __forceinline__ bool first_hit(const typename R::Ctx &ctx, V3 d, cons
     return false;
 }
 
-/* The spine's query (one ray, the same on every lane): every primitive's span
- * at once and the fast checks; where they hold, the first hit is a positive
- * primitive's own boundary -- its start (entry) if that is >= EPS, else its
- * end (exit, the pairs around it strictly separated), never a flipped one --
- * so the reference's ref and exit flag follow from the chosen primitive.
- * Otherwise the lazy merge, as before.  The checks are wave-uniform here. */
+/* First hit from every primitive's span at once, where the fast checks hold
+ * (the union rule in union-only trees, else the pairwise checks): the hit is
+ * then a positive primitive's own boundary -- its start (entry) if that is
+ * >= EPS, else its end (exit, the pairs around it strictly separated), never
+ * a flipped one -- so the reference's ref and exit flag follow from the
+ * chosen primitive.  Returns the check's verdict; the result is valid only
+ * where it holds. */
+template <class R, class PS>
+__device__ __forceinline__ int span_first_hit(const PS &ps, bool &hit, float &t, u32 &ref, bool &exit_hit)
+{
+    int fok;
+    if constexpr (R::UNION_ONLY)
+        fok = union_min_ok(ps, [&](auto &&f) { R::each_pos(f); }) || R::fast_ok(ps);
+    else
+        fok = R::fast_ok(ps);
+    int found = 0;
+    u32 bref = 0u;
+    float b0 = 0.0f, b1 = 0.0f;
+    R::each_pos([&](auto x, auto m) {
+        constexpr int X = decltype(x)::value;
+        const int cand = ps.live[X] & (ps.t1[X] >= EPS);
+        const int better = cand & ((!found) | (ps.t0[X] < b0));
+        b0 = better ? ps.t0[X] : b0;
+        b1 = better ? ps.t1[X] : b1;
+        bref = better ? mkref(X, decltype(m)::value, 0) : bref;
+        found |= cand;
+    });
+    hit = false;
+    if (found && b0 < MAXV) {
+        if (b0 >= EPS)
+            hit = true, t = b0, ref = bref, exit_hit = false;
+        else if (b1 < MAXV)
+            hit = true, t = b1, ref = bref | 2u, exit_hit = true; /* mkref(prim, mat, 1) */
+    }
+    return fok;
+}
+
+/* The spine's query (one ray, the same on every lane): span_first_hit where
+ * the checks hold, else the lazy merge.  The checks are wave-uniform here. */
 template <class R>
 __device__ __forceinline__ bool spine_first_hit(const typename R::Ctx &ctx, V3 d, const Env &e, float &t, u32 &ref,
                                                 bool &exit_hit)
 {
     PrimSpans<R::HI> ps;
     R::span(ps, ctx, mkray(d), e);
-    int fok;
-    if constexpr (R::UNION_ONLY)
-        fok = union_min_ok(ps, [&](auto &&f) { R::each_pos(f); }) || R::fast_ok(ps);
-    else
-        fok = R::fast_ok(ps);
-    if (!wave_any(!fok)) {
-        int found = 0;
-        u32 bref = 0u;
-        float b0 = 0.0f, b1 = 0.0f;
-        R::each_pos([&](auto x, auto m) {
-            constexpr int X = decltype(x)::value;
-            const int cand = ps.live[X] & (ps.t1[X] >= EPS);
-            const int better = cand & ((!found) | (ps.t0[X] < b0));
-            b0 = better ? ps.t0[X] : b0;
-            b1 = better ? ps.t1[X] : b1;
-            bref = better ? mkref(X, decltype(m)::value, 0) : bref;
-            found |= cand;
-        });
-        if (!found || b0 >= MAXV)
-            return false;
-        if (b0 >= EPS) {
-            t = b0, ref = bref, exit_hit = false;
-            return true;
-        }
-        if (b1 >= MAXV)
-            return false;
-        t = b1, ref = bref | 2u, exit_hit = true; /* mkref(prim, mat, 1) */
-        return true;
-    }
+    bool hit;
+    const int fok = span_first_hit<R>(ps, hit, t, ref, exit_hit);
+    if (!wave_any(!fok))
+        return hit;
     return first_hit<R>(ctx, d, e, t, ref, exit_hit);
+}
+
+/* A lane's own query (camera rays, lane-finished mirror children): the same,
+ * the lazy merge only on the lanes whose checks fail. */
+template <class R>
+__device__ __forceinline__ bool lane_first_hit(const typename R::Ctx &ctx, V3 d, const Env &e, float &t, u32 &ref,
+                                               bool &exit_hit)
+{
+#if defined(PT_FAST_SPINE) || defined(PT_FAST_LANE)
+    PrimSpans<R::HI> ps;
+    R::span(ps, ctx, mkray(d), e);
+    bool hit;
+    const int fok = span_first_hit<R>(ps, hit, t, ref, exit_hit);
+    if (wave_any(!fok)) {
+        if (!fok)
+            hit = first_hit<R>(ctx, d, e, t, ref, exit_hit);
+    }
+    return hit;
+#else
+    return first_hit<R>(ctx, d, e, t, ref, exit_hit);
+#endif
 }
 
 /* Fast first hit over precomputed primitive spans; valid when R::fast_ok. */
@@ -2368,7 +2397,7 @@ __device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 d, const
     u32 ref2 = 0;
     bool ex2 = false;
     V3 col = mk(0, 0, 0);
-    if (first_hit<typename S::Root>(ctx, refl, e, t2, ref2, ex2))
+    if (lane_first_hit<typename S::Root>(ctx, refl, e, t2, ref2, ex2))
         col = S::emis(ref_mat(ref2), hit + t2 * refl, e);
     res = (z + (retval + w * col)) / 1.0f;
     return true;
@@ -2633,7 +2662,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             typename S::Root::Ctx ctx;
             S::Root::prep(ctx, mk(0, 0, 0), e);
             bool ex = false;
-            ch.hit = first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
+            ch.hit = lane_first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
             ch.ex = ex ? 1 : 0;
             ldone = lane_sample<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
         }
