@@ -665,7 +665,7 @@ public:
         float screenWidth = 0, screenHeight = 0, screenDistance = 0; /* 0 = the demo's
                                        convention: W, H, 2 min(W, H) (src/test.cpp:450) */
         uint64_t seed = 0x5EED;     /* run seed of the per-(pixel, sample) engine   */
-        int order = PT_ORDER_GROUP64;
+        int order = PT_ORDER_FAST;
         int device = 0;
         int64_t maxBufferBytes = 0;
     };

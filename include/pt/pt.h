@@ -110,7 +110,9 @@ int pt_matrix_inverse(const float m[12], float out[12]);                /* PT_ER
 void pt_matrix_concat(const float a[12], const float b[12], float out[12]);
 
 /* ------------------------------------------------------------- render --- */
-#define PT_ORDER_GROUP64 0   /* fast path: leaf children summed in 64-wide pairwise groups */
+#define PT_ORDER_FAST 0      /* fast path: a burst's non-zero leaf-child terms dealt round-robin to 64
+                                lane sums, added as their pairwise tree; samples in
+                                32-sample pairwise blocks (oracle.cpp ORDER_FAST)     */
 #define PT_ORDER_REFERENCE 1 /* bit-for-bit the reference's sequential child order          */
 
 typedef struct pt_render_params {

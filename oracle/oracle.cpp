@@ -19,14 +19,19 @@
  *
  * Two accumulation orders:
  *   ORDER_REFERENCE : retval += child, one child at a time (path-trace.h:162)
- *   ORDER_GROUP64   : the GPU fast path's order -- in a scatter loop with
- *                     scatter_coefficient > eps, consecutive LEAF children
- *                     (depth-1 <= 0 or child strength < eps, i.e. children that
- *                     draw no random numbers) are summed in groups of up to 64
- *                     by a pairwise tree over 64 slots padded with -0.0f, and
- *                     each group total is added to retval; a non-leaf child
- *                     closes the open group and is added on its own.  A
- *                     pixel's samples are summed in blocks of 32 (pairwise
+ *   ORDER_FAST      : the GPU fast path's order -- in a scatter loop with
+ *                     scatter_coefficient > eps, a RUN is a maximal sequence of
+ *                     consecutive LEAF children (depth-1 <= 0 or child strength
+ *                     < eps, i.e. children that draw no random numbers).  The
+ *                     run's terms w * child that are not exactly zero (some
+ *                     channel != 0; NaN counts as non-zero) are dealt round-robin
+ *                     to 64 lane sums: the k-th such term of the run is added to
+ *                     lane k mod 64, each lane summing in order from +0.  Zero
+ *                     terms change no lane sum (a lane sum that starts at +0 is
+ *                     never -0), so where they fall does not matter.  At the run's
+ *                     end retval += the pairwise tree of the 64 lane sums; a
+ *                     non-leaf child closes the open run and is added on its own.
+ *                     A pixel's samples are summed in blocks of 32 (pairwise
  *                     tree each, padded with -0.0f), blocks one after the
  *                     other (pixel_sum).
  */
@@ -832,7 +837,7 @@ std::unique_ptr<Scene> load_scene(const std::string &text)
 }
 
 /* -------------------------------------------------------------- tracer --- */
-enum Order { ORDER_REFERENCE = 0, ORDER_GROUP64 = 1 };
+enum Order { ORDER_REFERENCE = 0, ORDER_FAST = 1 };
 
 /* uniform_real_distribution<float>::operator(), vector3d.h:22-33 */
 template <class E>
@@ -866,6 +871,39 @@ inline V3 pairwise64(const std::vector<V3> &g)
     return V3(b[0][0], b[1][0], b[2][0]);
 }
 
+/* The fast order's run of leaf children (ORDER_FAST above): non-zero terms
+ * dealt round-robin to 64 lane sums, flushed into retval as their pairwise
+ * tree.  An empty run adds nothing. */
+struct LaneSums
+{
+    float l[3][64];
+    int nz = 0, len = 0;
+    LaneSums() { reset(); }
+    void reset()
+    {
+        for (int c = 0; c < 3; c++)
+            for (int k = 0; k < 64; k++) l[c][k] = 0.0f;
+        nz = len = 0;
+    }
+    void add(V3 t)
+    {
+        len++;
+        if (t.x == 0.0f && t.y == 0.0f && t.z == 0.0f)
+            return;
+        const int k = nz++ & 63;
+        l[0][k] = l[0][k] + t.x, l[1][k] = l[1][k] + t.y, l[2][k] = l[2][k] + t.z;
+    }
+    void flush(V3 &retval)
+    {
+        if (!len)
+            return;
+        std::vector<V3> g(64);
+        for (int k = 0; k < 64; k++) g[k] = V3(l[0][k], l[1][k], l[2][k]);
+        retval = retval + pairwise64(g);
+        reset();
+    }
+};
+
 /* A pixel's sum of spp samples: in the reference order one after the other
  * (tracePixel, path-trace.h:192-199); in the group-64 order in blocks of 32
  * consecutive samples, each block its pairwise tree (missing leaves -0.0f),
@@ -875,7 +913,7 @@ template <class F>
 V3 pixel_sum(int spp, int order, F &&sample)
 {
     V3 acc(0, 0, 0);
-    if (order != ORDER_GROUP64) {
+    if (order != ORDER_FAST) {
         for (int s = 0; s < spp; s++) acc = acc + sample(s);
         return acc;
     }
@@ -974,8 +1012,8 @@ struct Tracer
         if (N == 0)
             N = 1;
         V3 rc = mat->reflect->color(hit);
-        std::vector<V3> group;
-        bool grouped = order == ORDER_GROUP64 && sc > kEps;
+        LaneSums run;
+        bool grouped = order == ORDER_FAST && sc > kEps;
         for (int i = 0; i < N; i++) {
             V3 refl = reflect(ray.d, n);
             V3 dir = refl;
@@ -984,8 +1022,7 @@ struct Tracer
                 do {
                     count++;
                     if (count > 1000) { /* path-trace.h:148-152 (NDEBUG semantics) */
-                        if (!group.empty())
-                            retval = retval + pairwise64(group);
+                        run.flush(retval);
                         return retval;
                     }
                     dir = rand_ball(rng);
@@ -1002,21 +1039,13 @@ struct Tracer
                 st.leaf_children++;
             V3 child = trace(Ray{ray.at(t), dir}, depth - 1, rng, cs);
             if (grouped && leaf) {
-                group.push_back(w * child);
-                if (group.size() == 64) {
-                    retval = retval + pairwise64(group);
-                    group.clear();
-                }
+                run.add(w * child);
             } else {
-                if (!group.empty()) {
-                    retval = retval + pairwise64(group);
-                    group.clear();
-                }
+                run.flush(retval);
                 retval = retval + w * child;
             }
         }
-        if (!group.empty())
-            retval = retval + pairwise64(group);
+        run.flush(retval);
         return retval;
     }
 
@@ -1139,7 +1168,7 @@ int oracle_render_adaptive(const char *scene_text, int W, int H, int spp, int de
         std::mutex mu;
         std::string err;
         auto worker = [&]() {
-            Tracer<SampleEngine> tr(*scene, order == 1 ? ORDER_GROUP64 : ORDER_REFERENCE);
+            Tracer<SampleEngine> tr(*scene, order == 1 ? ORDER_FAST : ORDER_REFERENCE);
             try {
                 for (;;) {
                     int k = next.fetch_add(1);
@@ -1152,7 +1181,7 @@ int oracle_render_adaptive(const char *scene_text, int W, int H, int spp, int de
                     b.valid.assign((size_t)(block + 1) * (block + 1), 0);
                     b.trace_pixel = [&](int px, int py) {
                         const uint64_t p = (uint64_t)py * gw + px;
-                        V3 acc = pixel_sum(spp, order == 1 ? ORDER_GROUP64 : ORDER_REFERENCE, [&](int s) {
+                        V3 acc = pixel_sum(spp, order == 1 ? ORDER_FAST : ORDER_REFERENCE, [&](int s) {
                             SampleEngine e(seed, p, (uint64_t)s);
                             return tr.sample(px, py, W, H, depth, sw, sh, dist, e);
                         });
@@ -1214,7 +1243,7 @@ int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int 
         Stats total;
         std::string err;
         auto worker = [&]() {
-            Tracer<SampleEngine> tr(*scene, order == 1 ? ORDER_GROUP64 : ORDER_REFERENCE);
+            Tracer<SampleEngine> tr(*scene, order == 1 ? ORDER_FAST : ORDER_REFERENCE);
             try {
                 for (;;) {
                     int k = next.fetch_add(1);
@@ -1222,7 +1251,7 @@ int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int 
                         break;
                     int p = pixels ? pixels[k] : k;
                     int px = p % gw, py = p / gw;
-                    V3 acc = pixel_sum(spp, order == 1 ? ORDER_GROUP64 : ORDER_REFERENCE, [&](int s) {
+                    V3 acc = pixel_sum(spp, order == 1 ? ORDER_FAST : ORDER_REFERENCE, [&](int s) {
                         SampleEngine e(seed, (uint64_t)p, (uint64_t)s);
                         V3 c = tr.sample(px, py, W, H, depth, sw, sh, dist, e);
                         if (per_sample) {

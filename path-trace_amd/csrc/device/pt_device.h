@@ -33,8 +33,9 @@
  * Arithmetic: compiled with -ffp-contract=off and correctly rounded f32
  * division/sqrt; every expression keeps the reference's evaluation order, so
  * per-sample radiance is bit-identical to the reference in PT_ORDER_REFERENCE
- * and to the oracle's group-64 order in the fast path (children of a burst
- * batch are summed by a 64-wide pairwise butterfly, padded with -0.0f).
+ * and to the oracle's fast order in the fast path (a burst's non-zero child
+ * terms dealt round-robin to 64 lane sums, added as their 64-wide pairwise
+ * tree).
  */
 #ifndef PT_DEVICE_H
 #define PT_DEVICE_H
@@ -335,6 +336,13 @@ __device__ __forceinline__ int lane_bit(u64 m)
     asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(r) : "s"(m));
     return r;
 }
+/* a where this lane's bit of the uniform mask m is set, else b: one v_cndmask on the mask */
+__device__ __forceinline__ int mask_sel(u64 m, int a, int b)
+{
+    int r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
 /* base + set bits of the uniform mask m in the lanes below this one (v_mbcnt) */
 __device__ __forceinline__ int mbcnt(u64 m, int base)
 {
@@ -389,7 +397,7 @@ __device__ __forceinline__ float wave_tree_sum(float v)
  * The row-broadcast levels add in place under a row mask (rows 1 and 3, then
  * row 3): the masked rows keep their value, as the -0.0 padding of
  * dpp_bcast_add does.  Same tree, same bits as wave_tree_sum (checked by the
- * GPU parity tests against the oracle's group-64 order).  Needs all 64 lanes
+ * GPU parity tests against the oracle's fast order).  Needs all 64 lanes
  * active. */
 __device__ __forceinline__ V3 wave_tree_sum3_add(V3 v, V3 acc)
 {
@@ -1533,8 +1541,8 @@ struct Counters
 {
     u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow, dark, mid;
 #ifdef PT_PHASE_TIMING
-    u64 ph[7]; /* cycles: generation, its attempts, fast pass, slow pass, group sums, burst total, sample total */
-    u64 np[8]; /* events: bursts, loop iterations, (unused), fast passes, slow passes, group sums, fast lanes, slow lanes */
+    u64 ph[7]; /* cycles: generation, its attempts, fast pass, slow pass, accumulation, burst total, sample total */
+    u64 np[8]; /* events: bursts, loop iterations, (unused), fast passes, slow passes, accumulations, fast lanes, slow lanes */
 #define PT_CNT(c, k, v) (c).np[k] += (v)
 #else
 #define PT_CNT(c, k, v)
@@ -1566,7 +1574,6 @@ __device__ __forceinline__ void cadd(u64 &c, u32 v)
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
-    unsigned char *flags; /* PT_FCAP child positions (mod): 1 = the child holds a ring slot */
     void *ctx;            /* the burst origin's S::Root::Ctx, prepared once per burst     */
     float4 *ring;         /* PT_RCAP kept-child slots: parked ray, then the child's term */
     unsigned char *slowq; /* PT_SCAP slots waiting for the full merge (ring number mod 256) */
@@ -1599,10 +1606,8 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #ifndef PT_KATT
 #define PT_KATT 8 /* rejection attempts per lane per generation round (A/B on C3: 4 -> 8 +6%) */
 #endif
-#define PT_RCAP 256  /* kept-child slots per wave awaiting their group sum            */
-#define PT_FCAP 2048 /* child-position flags per wave (32 groups of 64)               */
+#define PT_RCAP 256  /* kept-child slots per wave awaiting their lane-sum accumulation */
 #define PT_SCAP 128  /* mid / slow queue entries (< 128 pending by construction; byte ring numbers) */
-static_assert(64 * PT_KATT <= PT_FCAP / 2, "position flags too few for PT_KATT");
 static_assert(PT_KATT % 2 == 0, "deferred rounds evaluate attempts in pairs");
 #define PT_JUMP_ENTRIES 1025 /* host table: m = 0..1024 attempts */
 static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
@@ -1798,7 +1803,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
     float4 *const ring = L.ring;
-    unsigned char *const flags = L.flags, *const slowq = L.slowq, *const midq = L.midq;
+    unsigned char *const slowq = L.slowq, *const midq = L.midq;
     const int lane = threadIdx.x & 63;
     const u64 below = (1ull << lane) - 1ull;
     const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
@@ -1821,19 +1826,21 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     typename S::Root::Ctx c0;
     S::Root::prep(c0, hit, e);
     *cxp = c0;
-    /* Children are numbered by position in the burst (npos); positions 64g ..
-     * 64g + 63 form summation group g (the oracle's GROUP64 groups).  A DARK
-     * child (no emissive primitive reachable, positive weight) has the
-     * burst-uniform term Z = rc * 0: the generation round decides it on the
-     * accepted direction and it takes no memory beyond its position flag.
-     * Every other child is KEPT: the round parks its direction in the slot
-     * ring (numbered nkeep, in position order), where it waits for the fast
-     * pass and, if it fails the check there, the slow pass; flags[position]
-     * records which positions hold a ring slot. */
-    int npos = 0, nkeep = 0, keep_sum = 0, gsum = 0, f_n = 0, s_head = 0, s_n = 0, s_first = 0;
+    /* The burst's leaf children form one run of the fast order (oracle.cpp
+     * ORDER_FAST): the run's non-zero terms are dealt round-robin to 64 lane
+     * sums (lsum; the k-th one to lane k mod 64), which are added into retval
+     * as their pairwise tree when the burst ends.  A DARK child (no emissive
+     * primitive reachable, finite weight) has a zero term: the generation round
+     * decides it on the accepted direction and it takes no memory at all.  Every
+     * other child is KEPT: the round parks its direction in the slot ring
+     * (numbered nkeep, in child order), where it waits for the passes, which
+     * write its term back into the slot; slots are accumulated into the lane
+     * sums in ring order once every slot before them is resolved.  npos counts
+     * the burst's children.  In reference order (STRICT) every child is kept and
+     * its term added to retval one by one (path-trace.h:160-162). */
+    int npos = 0, nkeep = 0, keep_sum = 0, nzc = 0, f_n = 0, s_head = 0, s_n = 0, s_first = 0;
     int m_head = 0, m_n = 0, m_first = 0;
-    /* ((aN * factor) * rc) * (+0) == rc * (+0) bitwise for any finite aN * factor > 0 */
-    const V3 Z = rc * mk(0.0f, 0.0f, 0.0f);
+    V3 lsum = mk(0.0f, 0.0f, 0.0f);
     int fast_on = 1, clear_on = 1;
     /* the clear pass applies when every emissive primitive hangs off the root
      * through Unions and transforms only */
@@ -1842,15 +1849,20 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
      * saves the mid queue's second pass (C2 2.94 -> 3.37 Msamples/s) */
     constexpr bool CLEAR = S::Root::template clear_ok<Emissive<S>>() && !S::Root::UNION_ONLY;
     /* RAW: dark children are decided on the unnormalised direction (dark_mask,
-     * sound but conservative).  The Z shortcut also needs a factor >= +0, i.e.
+     * sound but conservative).  The zero term also needs a factor >= +0, i.e.
      * a computed dot(normalize(w), n) >= 0: accepted w have a computed
      * n.w > EPS and |w| <= 1 + |kR| (< 65), so the rounding of normalize and
      * dot (< 7e-5 here) cannot flip the sign.  Without RAW every child is kept
      * and the fast pass computes its exact term. */
-    constexpr bool RAW = DEFERRED && S::Root::template raw_ok<Emissive<S>>();
+    constexpr bool RAW = DEFERRED && !STRICT && S::Root::template raw_ok<Emissive<S>>();
     /* with the dark tests' burst-uniform preconditions folded in once per
-     * burst: AND_p (ballot_p & pre_p) == (AND_p ballot_p) & AND_p pre_p */
-    const u64 raw_mask = uni_mask((KR0 || length(kR) < 64.0f) && S::Root::template dark_pre<Emissive<S>>(c0, e));
+     * burst: AND_p (ballot_p & pre_p) == (AND_p ballot_p) & AND_p pre_p.  A dark
+     * child's term ((aN * factor) * rc) * (+0, +0, +0) is zero when the weight is
+     * finite: aN <= 1, factor <= 1 + 2^-20, so |rc| < 1e37 per channel suffices
+     * (NaN fails the compares: such bursts keep every child). */
+    const bool wfin = __builtin_fabsf(rc.x) < 1e37f && __builtin_fabsf(rc.y) < 1e37f && __builtin_fabsf(rc.z) < 1e37f;
+    const u64 raw_mask =
+        uni_mask((KR0 || length(kR) < 64.0f) && wfin && S::Root::template dark_pre<Emissive<S>>(c0, e));
     /* queued slots hold ring numbers mod 256; every pending one lies in
      * [keep_sum, keep_sum + PT_RCAP), which restores it */
     auto slot_pos = [&](unsigned char v) { return keep_sum + ((int)(v - keep_sum) & (PT_RCAP - 1)); };
@@ -1858,13 +1870,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     for (;;) {
         PT_CNT(cnt, 1, 1);
         /* a round needs 64 free ring slots (more kept children than free slots
-         * end the round early, below) and 64*PT_KATT free position flags */
-        const bool room = PT_RCAP - (nkeep - keep_sum) >= 64 && npos - 64 * gsum <= PT_FCAP - 64 * PT_KATT;
+         * end the round early, below) */
+        const bool room = PT_RCAP - (nkeep - keep_sum) >= 64;
         if (reason < 0 && room) {
             PT_T0(tg);
             PT_MARK(13);
             /* ---- generation round: lane l evaluates attempts l, 64 + l, ...
-             * Each attempt's flag and ring entry are written at once, as if
+             * Each kept attempt's ring entry is written at once, as if
              * the whole round were consumed: a round that stops early consumes
              * a prefix of the accepted attempts, whose writes are the same, and
              * the rest lie past npos / nkeep, where nothing reads them before
@@ -1880,14 +1892,10 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 #endif
             int ta = 0, tk = 0; /* accepted / kept attempts of the round */
             u64 nlor = 0ull, Alast = 0ull, Flast = 0ull;
-            /* one attempt's flag and (kept, with a free slot) ring entry */
-            auto write_attempt = [&](bool acc, u64 A, u64 kp, V3 wn, float factor) {
-                /* two flat lane-conditional stores, not nested ones (kp is a
-                 * subset of A): one exec round trip fewer per attempt */
+            /* one attempt's ring entry (kept, with a free slot) */
+            auto write_attempt = [&](u64 A, u64 kp, V3 wn, float factor) {
                 const int kl = lane_bit(kp);
                 const int ko = mbcnt(kp, tk);
-                if (acc)
-                    flags[mbcnt(A, npos + ta) & (PT_FCAP - 1)] = (unsigned char)kl;
                 if (kl && ko < free_slots)
                     ring[(nkeep + ko) & (PT_RCAP - 1)] = make_float4(wn.x, wn.y, wn.z, factor);
                 ta += __popcll(A);
@@ -1909,7 +1917,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         u64 D = 0ull;
                         if (RAW)
                             D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
-                        write_attempt(ap.acc[h], ap.A[h], ap.A[h] & ~D, wn, 0.0f);
+                        write_attempt(ap.A[h], ap.A[h] & ~D, wn, 0.0f);
                         if (k + h == PT_KATT - 1)
                             Alast = ap.A[h], Flast = ap.F[h];
                     }
@@ -1921,7 +1929,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     if (k)
                         sk = A64 * sk + g64inc;
                     const Attempt at = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
-                    write_attempt(at.acc, at.A, at.A, at.wn, at.factor);
+                    write_attempt(at.A, at.A, at.wn, at.factor);
                     nlor |= at.NL;
                     if (k == PT_KATT - 1)
                         Alast = at.A, Flast = at.F;
@@ -2033,8 +2041,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
         }
         const bool final = reason >= 0;
         /* drain everything when the next round would not fit */
-        const bool drain =
-            final || PT_RCAP - (nkeep - keep_sum) < 64 || npos - 64 * gsum > PT_FCAP - 64 * PT_KATT;
+        const bool drain = final || PT_RCAP - (nkeep - keep_sum) < 64;
         /* The fast check of one kept child (its normalised direction and
          * factor in en): true when its term is written to the ring, false
          * when it needs the full merge. */
@@ -2219,71 +2226,51 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             break;
         }
         PT_T0(ts);
-        /* ---- sum finished groups in order: 64 children per group (the last
-         * group of a burst may be shorter), group-64 tree or sequential; a
-         * group is finished when all its positions are consumed and every
-         * kept child in it has its term */
+        /* ---- accumulate resolved slots in ring order: 64 at a time, fewer
+         * only when draining.  Fast order: the batch's non-zero terms go to the
+         * next lanes of the round-robin (lane (nzc + j) mod 64 for the batch's
+         * j-th one) by one forward permute; the zero terms fill the remaining
+         * lanes, where adding +-0 changes nothing (a lane sum starting at +0 is
+         * never -0). */
         {
             int resolved = nkeep - f_n;
             if (m_n)
                 resolved = min(resolved, m_first);
             if (s_n)
                 resolved = min(resolved, s_first);
-            const int ngrp = final ? (npos + 63) >> 6 : npos >> 6;
-            while (gsum < ngrp) {
-                const int cg = min(64, npos - 64 * gsum);
-                const bool kl = lane < cg && flags[(64 * gsum + lane) & (PT_FCAP - 1)];
-                const u64 gm = __ballot(kl);
-                const int gk = __popcll(gm);
-                if (keep_sum + gk > resolved)
-                    break;
+            while (resolved - keep_sum >= 64 || (drain && resolved > keep_sum)) {
+                const int c = min(64, resolved - keep_sum);
                 PT_CNT(cnt, 5, 1);
-                V3 term = mk(-0.0f, -0.0f, -0.0f);
-                if (lane < cg)
-                    term = Z;
-                if (kl) {
-                    const float4 tv = ring[mbcnt(gm, keep_sum) & (PT_RCAP - 1)];
-                    term = mk(tv.x, tv.y, tv.z);
-                }
-                if (!STRICT && gsum + 1 < ngrp) {
-                    /* groups finish in batches (a slow pass resolves many at
-                     * once): when the next group is finished too, its tree
-                     * sums run right after these; retval still adds the group
-                     * sums one after the other */
-                    const int cg2 = min(64, npos - 64 * (gsum + 1));
-                    const bool kl2 = lane < cg2 && flags[(64 * (gsum + 1) + lane) & (PT_FCAP - 1)];
-                    const u64 gm2 = __ballot(kl2);
-                    const int gk2 = __popcll(gm2);
-                    if (keep_sum + gk + gk2 <= resolved) {
-                        PT_CNT(cnt, 5, 1);
-                        V3 term2 = mk(-0.0f, -0.0f, -0.0f);
-                        if (lane < cg2)
-                            term2 = Z;
-                        if (kl2) {
-                            const float4 tv = ring[mbcnt(gm2, keep_sum + gk) & (PT_RCAP - 1)];
-                            term2 = mk(tv.x, tv.y, tv.z);
-                        }
-                        retval = wave_tree_sum3_add(term, retval);
-                        retval = wave_tree_sum3_add(term2, retval);
-                        keep_sum += gk + gk2;
-                        gsum += 2;
-                        continue;
-                    }
+                V3 t = mk(0.0f, 0.0f, 0.0f);
+                if (lane < c) {
+                    const float4 tv = ring[(keep_sum + lane) & (PT_RCAP - 1)];
+                    t = mk(tv.x, tv.y, tv.z);
                 }
                 if (STRICT) {
-                    for (int j = 0; j < cg; j++)
-                        retval = retval + mk(rdlane(term.x, j), rdlane(term.y, j), rdlane(term.z, j));
+                    for (int j = 0; j < c; j++)
+                        retval = retval + mk(rdlane(t.x, j), rdlane(t.y, j), rdlane(t.z, j));
                 } else {
-                    retval = wave_tree_sum3_add(term, retval);
+                    /* NaN compares unequal: a NaN term counts as non-zero, as in the oracle */
+                    const u64 nz = __ballot(t.x != 0.0f) | __ballot(t.y != 0.0f) | __ballot(t.z != 0.0f);
+                    const int pnz = __popcll(nz);
+                    const int k = mask_sel(nz, mbcnt(nz, nzc), mbcnt(~nz, nzc + pnz));
+                    const int to = (k & 63) << 2;
+                    t = mk(__int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(t.x))),
+                           __int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(t.y))),
+                           __int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(t.z))));
+                    lsum = lsum + t;
+                    nzc += pnz;
                 }
-                keep_sum += gk;
-                gsum++;
+                keep_sum += c;
             }
         }
         PT_ACC(cnt, 4, ts);
         if (final)
             break;
     }
+    /* the run's end: retval + the pairwise tree of the 64 lane sums */
+    if (!STRICT && npos > 0)
+        retval = wave_tree_sum3_add(lsum, retval);
     f.retval = retval;
     f.i = i + npos;
     return reason;
@@ -2612,7 +2599,6 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                                              const PtLaunch &lp)
 {
     __shared__ Frame stk[PT_WPW][MAXD + 1];
-    __shared__ unsigned char pbuf[PT_WPW][PT_FCAP];
     __shared__ typename S::Root::Ctx xbuf[PT_WPW];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
     __shared__ unsigned char sbuf[PT_WPW][PT_SCAP];
@@ -2631,7 +2617,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
 #endif
-    const WaveLds L = {pbuf[wave], &xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave]};
+    const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
@@ -2692,7 +2678,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         if (lp.block_sums) {
             /* the chunk is one 32-sample block of one slot (slot-major, chunk
              * 32, nsamp % 32 == 0): its 32-leaf pairwise tree is the block
-             * partial of the group-64 order's pixel sum.  Level w adds lane
+             * partial of the fast order's pixel sum.  Level w adds lane
              * k + w into lane k, so lane 0 ends with pt_tree32's association.
              * The three sums are read out of lane 0 here, at full exec, and
              * lanes 0-2 store one channel each: a read of lane 0 inside a
@@ -2750,7 +2736,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
 template <class S, int MAXD>
 __device__ constexpr int min_workgroups()
 {
-    constexpr int lds = PT_WPW * ((MAXD + 1) * (int)sizeof(Frame) + PT_FCAP + 16 * PT_RCAP + 2 * PT_SCAP +
+    constexpr int lds = PT_WPW * ((MAXD + 1) * (int)sizeof(Frame) + 16 * PT_RCAP + 2 * PT_SCAP +
                                   (int)sizeof(Counters) + (int)sizeof(typename S::Root::Ctx));
     constexpr int alloc = (lds + 1279) / 1280 * 1280; /* gfx950 LDS allocation unit (measured) */
     constexpr int n = 160 * 1024 / alloc;
@@ -2787,10 +2773,10 @@ __device__ constexpr int min_workgroups()
  * accum; on the last pass acc / spp goes to the frame buffer.
  *   mode 0 (reference order): acc = ((acc + x_0) + x_1) + ..., tracePixel's
  *          own accumulation (path-trace.h:192-199), from per-sample values;
- *   mode 1 (group-64 order, per-sample stage): samples in blocks of 32 from
+ *   mode 1 (fast order, per-sample stage): samples in blocks of 32 from
  *          the call's first sample, each block its 32-leaf pairwise tree
  *          (missing leaves -0.0f), acc = ((acc + B_0) + B_1) + ...;
- *   mode 2 (group-64 order, block stage): the same with the block partials
+ *   mode 2 (fast order, block stage): the same with the block partials
  *          already summed by the render kernel (one per 32 samples). */
 __device__ __forceinline__ float pt_tree32(const float *v, int n, int stride)
 {

@@ -10,7 +10,7 @@
  *   slot-major for large launches, sample-major for launches of <= 64 samples
  *   per slot.  Reference order stages each sample's radiance and pt_reduce
  *   sums a pixel's samples in sample order, exactly tracePixel's loop; the
- *   group-64 order stages one pairwise partial per 32-sample block (whole
+ *   fast order stages one pairwise partial per 32-sample block (whole
  *   blocks per chunk) or per-sample values, and pt_reduce adds the blocks in
  *   order.  Large frames run in sample passes bounded by max_buffer_bytes,
  *   the running per-pixel sums carried between passes.
@@ -491,7 +491,7 @@ void validate(const pt_render_params *p)
         throw Error(PT_ERR_ARG, "samples must lie in [0, 2^20) (engine key layout)");
     if (p->depth < 0 || p->depth > 64)
         throw Error(PT_ERR_ARG, "depth must be in [0, 64]");
-    if (p->order != PT_ORDER_GROUP64 && p->order != PT_ORDER_REFERENCE)
+    if (p->order != PT_ORDER_FAST && p->order != PT_ORDER_REFERENCE)
         throw Error(PT_ERR_ARG, "bad order");
     if (p->grid_width != 0 && p->grid_width < p->width)
         throw Error(PT_ERR_ARG, "grid_width must be 0 or >= width");
@@ -512,7 +512,7 @@ size_t frame_floats(const pt_render_params *p)
     return 3 * n;
 }
 
-/* The group-64 order sums a pixel's samples in blocks of 32 (pt_device.h
+/* The fast order sums a pixel's samples in blocks of 32 (pt_device.h
  * pt_reduce); a slot-major launch of whole blocks stages one partial per
  * block instead of one value per sample (32x less: C4 3.2 GB, C5 25 GB in one
  * pass). */
@@ -525,7 +525,7 @@ bool block_staging(const pt_render_params *p)
         fprintf(stderr, "pt: experiment hook PT_BLOCK_SUMS=%s active\n", env);
         return atoi(env) == 0;
     }();
-    return !off && p->order == PT_ORDER_GROUP64 && p->spp > 64 && p->spp % 32 == 0;
+    return !off && p->order == PT_ORDER_FAST && p->spp > 64 && p->spp % 32 == 0;
 }
 
 long long pass_samples(const pt_render_params *p, long long npix)

@@ -18,7 +18,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import PT_ORDER_GROUP64, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, load_hdr, load_png, \
+from ._lib import PT_ORDER_FAST, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, load_hdr, load_png, \
     write_bmp, write_hdr
 from .scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTexture, ImageSkyboxAlphaTexture,
                     ImageSkyboxTexture, ImageTexture, Intersection, LogTexture, Material, Matrix,
@@ -28,7 +28,7 @@ from .scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTex
 
 __all__ = [n for n in dir() if not n.startswith("_")] + ["DeviceScene", "render", "render_device", "prepare"]
 
-ORDERS = {"fast": PT_ORDER_GROUP64, "group64": PT_ORDER_GROUP64, "reference": PT_ORDER_REFERENCE,
+ORDERS = {"fast": PT_ORDER_FAST, "reference": PT_ORDER_REFERENCE,
           "strict": PT_ORDER_REFERENCE}
 
 

@@ -12,7 +12,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(HERE, "..", "lib", "libpt.so"))
 
-PT_ORDER_GROUP64 = 0
+PT_ORDER_FAST = 0
 PT_ORDER_REFERENCE = 1
 PT_CSG_UNION, PT_CSG_INTERSECTION, PT_CSG_DIFFERENCE = 0, 1, 2
 

@@ -87,7 +87,7 @@ def _tracer(txt, W, H, spp, depth, block):
     gw = (W + block - 1) // block * block + 1
     rows = (H + block - 1) // block * block + 1
     grid = O.render_gw(txt, W, H, gw, np.arange(gw * rows), spp, depth,
-                       order=O.ORDER_GROUP64).reshape(rows, gw, 3)
+                       order=O.ORDER_FAST).reshape(rows, gw, 3)
     return lambda x, y: grid[y, x].copy()
 
 
@@ -96,7 +96,7 @@ def _tracer(txt, W, H, spp, depth, block):
 def test_oracle_adaptive_matches_python_restatement(built, tmp_path, W, H, block, max_interp, delta):
     txt = to_text(scenes.scene_p1(), str(tmp_path))
     spp, depth = 2, 4
-    got, traced = O.render_adaptive(txt, W, H, spp, depth, block, max_interp, delta, order=O.ORDER_GROUP64)
+    got, traced = O.render_adaptive(txt, W, H, spp, depth, block, max_interp, delta, order=O.ORDER_FAST)
     want = py_adaptive(_tracer(txt, W, H, spp, depth, block), W, H, block, max_interp, delta)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
     assert 0 < traced
@@ -108,9 +108,9 @@ def test_oracle_adaptive_without_interpolation_is_per_pixel(built, tmp_path):
     W, H = 37, 21
     gw = 41  # ceil(37 / 8) * 8 + 1
     txt = to_text(T.csg_zoo(), str(tmp_path))
-    got, _ = O.render_adaptive(txt, W, H, 2, 4, 8, 1, 0.003, order=O.ORDER_GROUP64)
+    got, _ = O.render_adaptive(txt, W, H, 2, 4, 8, 1, 0.003, order=O.ORDER_FAST)
     ys, xs = np.mgrid[0:H, 0:W]
-    want = O.render_gw(txt, W, H, gw, (ys * gw + xs).ravel(), 2, 4, order=O.ORDER_GROUP64)
+    want = O.render_gw(txt, W, H, gw, (ys * gw + xs).ravel(), 2, 4, order=O.ORDER_FAST)
     np.testing.assert_array_equal(got.reshape(-1, 3).view(np.uint32), want.view(np.uint32))
 
 
@@ -123,7 +123,7 @@ def test_gpu_adaptive_matches_oracle(built, tmp_path, builder, W, H, spp, depth,
     img, info = pt.render_adaptive(root, W, H, spp, depth, block_size=block, max_interp=max_interp,
                                    min_delta=delta)
     want, traced = O.render_adaptive(to_text(root, str(tmp_path)), W, H, spp, depth, block, max_interp, delta,
-                                     order=O.ORDER_GROUP64)
+                                     order=O.ORDER_FAST)
     diff = np.nonzero(img.reshape(-1, 3).view(np.uint32) != want.reshape(-1, 3).view(np.uint32))[0]
     assert diff.size == 0, "%d mismatches, first %s" % (diff.size, diff[:4])
     # the GPU traces each distinct pixel once; the oracle once per block that needs it

@@ -43,7 +43,7 @@ def _worker(rank, world, port, txt, W, H, spp, depth, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pix = ptdist.rank_pixels(W, H, rank, world, tile=4)
     fb = torch.zeros(W * H * 3, dtype=torch.float32)
-    vals = O.render(txt, W, H, spp, depth, pixels=pix, threads=2, order=O.ORDER_GROUP64)
+    vals = O.render(txt, W, H, spp, depth, pixels=pix, threads=2, order=O.ORDER_FAST)
     fb.view(-1, 3)[torch.from_numpy(pix.astype(np.int64))] = torch.from_numpy(vals)
     ptdist.reduce_frame(fb)
     if rank == 0:
@@ -61,7 +61,7 @@ def test_gloo_two_ranks_bitexact(built, tmp_path):
     out = str(tmp_path / "fb.npy")
     mp.spawn(_worker, args=(2, _free_port(), txt, W, H, spp, depth, out), nprocs=2, join=True)
     got = np.load(out).reshape(-1, 3)
-    want = O.render(txt, W, H, spp, depth, order=O.ORDER_GROUP64)
+    want = O.render(txt, W, H, spp, depth, order=O.ORDER_FAST)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
@@ -72,7 +72,7 @@ def _split_worker(rank, world, port, txt, W, H, spp, depth, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     b, e = rank * spp // world, (rank + 1) * spp // world
-    per = O.render(txt, W, H, spp, depth, threads=2, order=O.ORDER_GROUP64, per_sample=True)[:, b:e]
+    per = O.render(txt, W, H, spp, depth, threads=2, order=O.ORDER_FAST, per_sample=True)[:, b:e]
     acc = np.zeros((W * H, 3), dtype=np.float32)
     for s in range(per.shape[1]):  # this rank's samples, summed in sample order (sum_only)
         acc = (acc + per[:, s]).astype(np.float32)
@@ -98,7 +98,7 @@ def test_gloo_sample_split_two_ranks(built, tmp_path):
     out = str(tmp_path / "fb.npy")
     mp.spawn(_split_worker, args=(2, _free_port(), txt, W, H, spp, depth, out), nprocs=2, join=True)
     got = np.load(out).reshape(-1, 3).astype(np.float64)
-    want = O.render(txt, W, H, spp, depth, order=O.ORDER_GROUP64).astype(np.float64)
+    want = O.render(txt, W, H, spp, depth, order=O.ORDER_FAST).astype(np.float64)
     rmse = np.sqrt(np.mean((got - want) ** 2, axis=0))
     assert np.all(rmse < 1e-6), rmse
     assert np.abs(got - want).max() <= 1e-6 * max(1.0, np.abs(want).max())

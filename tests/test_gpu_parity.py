@@ -5,7 +5,7 @@ sources) and the CPU oracle.
 Bars (BASELINE.json north_star: per-channel RMSE <= 1e-3 on the float
 accumulator before tone mapping) -- checked here much more strictly:
   * PT_ORDER_REFERENCE : pixel means bit-identical to the reference's;
-  * PT_ORDER_GROUP64   : bit-identical to the oracle in the group-64 order,
+  * PT_ORDER_FAST   : bit-identical to the oracle in the fast order,
                          RMSE vs the reference <= 1e-5.
 """
 import os
@@ -51,7 +51,7 @@ def tree32(v):
 
 
 def block_sum(per):
-    """the group-64 order's pixel sum of per-sample values (npx x n x 3):
+    """the fast order's pixel sum of per-sample values (npx x n x 3):
     blocks of 32 samples, pairwise tree each, blocks added in order"""
     acc = np.zeros((per.shape[0], 3), dtype=np.float32)
     for s in range(0, per.shape[1], 32):
@@ -91,8 +91,8 @@ def test_fast_order_bitexact_vs_oracle_and_within_bar(built, tmp_path, case):
     name, builder, W, H, spp, depth = case
     root = T.build(builder)
     g = pt.render(root, W, H, spp, depth, order="fast")
-    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_GROUP64)
-    assert_bits(g, o, "fast order vs oracle group64")
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_FAST)
+    assert_bits(g, o, "fast order vs oracle fast order")
     e = rmse(g.reshape(-1, 3), golden_means(name))
     assert np.all(e <= RMSE_BAR) and np.all(e <= 1e-5), e
 
@@ -106,7 +106,7 @@ def test_union_rule_overlaps_and_ties_bitexact(built, tmp_path, order):
     W, H, spp, depth = 48, 32, 4, 6
     g = pt.render(root, W, H, spp, depth, order=order)
     o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth,
-                 order=O.ORDER_GROUP64 if order == "fast" else O.ORDER_REFERENCE)
+                 order=O.ORDER_FAST if order == "fast" else O.ORDER_REFERENCE)
     assert_bits(g, o, "union zoo, %s order vs oracle" % order)
 
 
@@ -118,7 +118,7 @@ def test_fast_spine_bitexact(built, tmp_path, builder, depth):
     root = T.build(builder)
     W, H, spp = 40, 24, 3
     g = pt.render(pt.DeviceScene(root, fast_spine=True), W, H, spp, depth, order="fast")
-    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_GROUP64)
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_FAST)
     assert_bits(g, o, "fast spine, %s vs oracle" % builder)
 
 
@@ -131,7 +131,7 @@ def test_full_1080p_frame_on_sampled_pixels(built, tmp_path):
     rng = np.random.default_rng(7)
     pix = np.sort(rng.choice(cfg.width * cfg.height, 1500, replace=False)).astype(np.int32)
     o = O.render(to_text(root, str(tmp_path)), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen,
-                 pixels=pix, order=O.ORDER_GROUP64)
+                 pixels=pix, order=O.ORDER_FAST)
     assert_bits(img.reshape(-1, 3)[pix], o, "1080p sample")
     assert st["samples"] == cfg.width * cfg.height * 2
     assert 300 < st["queries"] / st["samples"] < 2000
@@ -150,7 +150,7 @@ def test_benchmark_configs_on_sampled_pixels(built, tmp_path, name, spp, npix):
     rng = np.random.default_rng(11)
     pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
     o = O.render(to_text(root, str(tmp_path)), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen,
-                 pixels=pix, order=O.ORDER_GROUP64)
+                 pixels=pix, order=O.ORDER_FAST)
     assert_bits(img.reshape(-1, 3)[pix], o, "%s sample" % name)
 
 
@@ -182,7 +182,7 @@ def test_virtual_ranks_on_one_gpu_sum_to_full_frame(built):
 def test_edge_shapes_and_depths(built, tmp_path, W, H, spp, depth):
     root = T.csg_zoo()
     g = pt.render(root, W, H, spp, depth)
-    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_GROUP64)
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_FAST)
     assert_bits(g, o, "edge %dx%d spp %d depth %d" % (W, H, spp, depth))
 
 
@@ -233,7 +233,7 @@ def test_round_cut_paths_bitexact(built, tmp_path, monkeypatch, cap):
     root = scenes.scene_p1()
     W, H, spp, depth = 40, 24, 6, 8
     g = pt.render(root, W, H, spp, depth)
-    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_GROUP64)
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_FAST)
     assert_bits(g, o, "PT_ROOM_CAP=%d" % cap)
 
 
@@ -263,21 +263,21 @@ def test_c4_eight_shards_on_one_gpu(built, tmp_path):
     rng = np.random.default_rng(44)
     pix = np.sort(rng.choice(W * H, 800, replace=False)).astype(np.int32)
     o = O.render(to_text(root, str(tmp_path)), W, H, spp, cfg.depth, screen=cfg.screen, pixels=pix,
-                 order=O.ORDER_GROUP64)
+                 order=O.ORDER_FAST)
     assert_bits(acc[pix], o, "8 shards vs oracle")
 
 
 def test_sample_split_sums(built, tmp_path):
     """bench.py's N-GPU sample split: a call renders samples sample_begin ..
     sample_begin + spp - 1 of every pixel and (sum_only) writes their sum in
-    the group-64 order's pixel order (blocks of 32 from the call's first
+    the fast order's pixel order (blocks of 32 from the call's first
     sample, pairwise tree each, blocks in order); the oracle's per-sample
     values summed the same way match bit for bit, and the ranks' sums added
     and divided by the total spp stay within float rounding of the
     single-call frame."""
     root = scenes.scene_p1()
     W, H, S, depth = 40, 24, 12, 8
-    per = O.render(to_text(root, str(tmp_path)), W, H, S, depth, order=O.ORDER_GROUP64, per_sample=True)
+    per = O.render(to_text(root, str(tmp_path)), W, H, S, depth, order=O.ORDER_FAST, per_sample=True)
     ds = pt.DeviceScene(root)
     total = np.zeros((W * H, 3), dtype=np.float32)
     for b, c in [(0, 5), (5, 4), (9, 3)]:
@@ -300,7 +300,7 @@ def test_config_scale_vs_reference(built, name, tmp_path):
     RMSE 1e-5 -- except C5, whose 8192-sample pixel sums the reference adds
     sequentially: there the reference itself is 3.9e-5 RMSE from the float64
     mean and the fast order's 32-sample blocks 5e-7, so the fast
-    order is held to the oracle's group-64 order at 1e-5 and to the reference
+    order is held to the oracle's fast order at 1e-5 and to the reference
     at 1e-4 (the north star's bar is 1e-3)."""
     z = np.load(os.path.join(GOLD, "config_%s.npz" % name))
     pix, ref = z["pixels"], z["means"]
@@ -318,7 +318,7 @@ def test_config_scale_vs_reference(built, name, tmp_path):
     bar = 1e-5
     if name == "C5":
         o = O.render(to_text(cfg.scene(), str(tmp_path)), W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix,
-                     order=O.ORDER_GROUP64)
+                     order=O.ORDER_FAST)
         e = rmse(f, o)
         assert np.all(e <= 1e-5), e
         assert np.isclose(f, o, rtol=1e-5, atol=1e-7).all(axis=1).mean() >= 0.95
@@ -332,7 +332,7 @@ def test_block_staged_pixel_sums(built, tmp_path):
     resident wave) stage one partial per block, the chunk's 32 samples summed
     by the DPP tree; passes of 64 samples stage per-sample values and pt_reduce
     forms the blocks.  Both bit-identical to each other on every pixel and to
-    the oracle's group-64 order (and a numpy restatement of the pixel sum) on
+    the oracle's fast order (and a numpy restatement of the pixel sum) on
     hashed pixels."""
     root = scenes.scene_p1()
     W, H, spp, depth = 256, 160, 128, 8
@@ -345,7 +345,7 @@ def test_block_staged_pixel_sums(built, tmp_path):
     rng = np.random.default_rng(3)
     pix = np.sort(rng.choice(W * H, 300, replace=False)).astype(np.int32)
     txt = to_text(root, str(tmp_path))
-    o = O.render(txt, W, H, spp, depth, pixels=pix, order=O.ORDER_GROUP64)
-    per = O.render(txt, W, H, spp, depth, pixels=pix, order=O.ORDER_GROUP64, per_sample=True)
+    o = O.render(txt, W, H, spp, depth, pixels=pix, order=O.ORDER_FAST)
+    per = O.render(txt, W, H, spp, depth, pixels=pix, order=O.ORDER_FAST, per_sample=True)
     assert_bits(block_sum(per) / np.float32(spp), o, "numpy block sums vs oracle")
     assert_bits(one.reshape(-1, 3)[pix], o, "block-staged vs oracle")

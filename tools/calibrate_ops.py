@@ -34,7 +34,7 @@ if __name__ == "__main__":
     pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
     txt = to_text(cfg.scene(), "/tmp/pt_calib_img")
     _, st = O.render(txt, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, pixels=pix, stats=True,
-                     order=O.ORDER_GROUP64)
+                     order=O.ORDER_FAST)
     ops = model_ops(st)
     print(json.dumps({"config": name, "pixels": npix, "spp": spp, "queries_per_sample": st["queries"] / (npix * spp),
                       "ops_per_query": ops / st["queries"], "ops_per_sample": ops / (npix * spp), **st}))
