@@ -43,14 +43,16 @@ OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 614.78, "C5": 554.13}
 # Counter evidence of this same command (tools/pmc_bench.sh: rocprofv3 --pmc
 # passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 + WRITE_SIZE)
 PMC_JSON = os.path.join(ROOT, "profiles", "round2", "pmc_bench_%s.json")
-# bounded CPU samples (~10-30 s of reference work on the box's 16 host threads)
-CPU_PIXELS = {"C1": 2048, "C2": 512, "C3": 2048, "C4": 2048, "C5": 32768}
-# C5 (3840x2160 x 8192 spp, 68 G samples) is timed on a hashed pixel subset at
-# its full spp and depth: at that size the reference camera (|d| = 4320) hides
-# everything nearer than 4.32 units, so the frame is the sky box, the skybox
-# sphere and the far side of the glass ball (~6 % of pixels, ~60x the cost of a
-# sky pixel); a hashed subset of 65536 pixels holds the same mix
-SUBSET = {"C5": 65536}
+# bounded CPU samples at full spp on the box's per-GPU CPU share (16 threads):
+# BASELINE.md's 4096 hashed pixels (C3: ~60 s), fewer where a pixel costs more
+CPU_PIXELS = {"C1": 4096, "C2": 512, "C3": 4096, "C4": 1024, "C5": 32768}
+# C5 (3840x2160 x 8192 spp, 68 G samples) is timed on one GPU on a hashed pixel
+# subset at its full spp and depth: at that size the reference camera
+# (|d| = 4320) hides everything nearer than 4.32 units, so the frame is the sky
+# box, the skybox sphere and the far side of the glass ball (~6 % of pixels,
+# ~60x the cost of a sky pixel); a hashed subset of 65536 pixels holds the same
+# mix.  On N > 1 GPUs the whole frame is rendered.
+SUBSET_1GPU = {"C5": 65536}
 
 
 def pmc_evidence(cfg_name: str):
@@ -70,7 +72,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=0, help="override (for quick local probes only; invalid metric)")
     ap.add_argument("--cpu-pixels", type=int, default=0, help="0 = the config's bounded sample (CPU_PIXELS)")
     ap.add_argument("--subset", type=int, default=-1,
-                    help="render only this many hashed pixels at full spp (-1 = config default, 0 = whole frame)")
+                    help="render only this many hashed pixels at full spp (-1 = config default: a subset for C5 on "
+                         "one GPU, else the whole frame; 0 = whole frame)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS "
                          "when set (the GPU box exports its per-GPU CPU share there)")
@@ -123,10 +126,17 @@ def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps, within=None):
         secs = time.time() - t0
         qps = st["queries"] / (npix * spp)
     value = npix * spp / secs / 1e6
+    host = len(os.sched_getaffinity(0))
     out = {"value": round(value, 5), "unit": "Msamples/s", "cores": threads, "kind": kind,
-           "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+           "host_cpus": os.cpu_count(), "affinity_cpus": host,
            "sample": "%d hashed pixels x %d spp of the same frame (%.1f s)" % (npix, spp, secs),
            "sample_queries_per_sample": round(qps, 2)}
+    if host > threads:
+        # the reference pool spawns hardware_concurrency() threads (src/test.cpp:204); the
+        # GPU box asks for its per-GPU CPU share only, so the whole host is a projection
+        # (pixels are independent: the pool scales linearly until memory bandwidth binds)
+        out["all_host_cpus_projected"] = {"value": round(value * host / threads, 5), "cores": host,
+                                          "how": "linear from the measured %d threads (not measured)" % threads}
     if frame_qps:
         out["frame_queries_per_sample"] = round(frame_qps, 2)
         out["value_rescaled_to_frame"] = round(value * qps / frame_qps, 5)
@@ -157,31 +167,28 @@ def main():
     W, H = cfg.width, cfg.height
     root = cfg.scene()
     ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine)
-    subset = SUBSET.get(cfg.name, 0) if args.subset < 0 else args.subset
-    by_samples = world > 1 and args.split == "samples"
-    mine = ptdist.rank_pixels(W, H, rank, 1 if by_samples else world)
-    s_begin, s_count = (rank * spp // world, (rank + 1) * spp // world - rank * spp // world) if by_samples \
-        else (0, spp)
+    subset = (SUBSET_1GPU.get(cfg.name, 0) if world == 1 else 0) if args.subset < 0 else args.subset
+    keep = None
     if subset:
         rng = np.random.default_rng(0x5EED)
         keep = np.sort(rng.choice(W * H, subset, replace=False)).astype(np.int32)
-        mine = np.intersect1d(mine, keep).astype(np.int32)
+    # this rank's share (pathtrace.dist.RankFrame, also driven by tests/test_dist_gpu.py)
+    share = ptdist.RankFrame(ds, W, H, spp, cfg.depth, rank=rank, world=world, split=args.split,
+                             screen=cfg.screen, subset=keep, order=args.order, device=local,
+                             max_buffer_bytes=40 << 30)
+    by_samples, mine = share.by_samples, share.pixels
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream()
-    params, keep = pt.make_params(W, H, s_count, cfg.depth, screen=cfg.screen, order=args.order, device=local,
-                                  pixels=None if ((world == 1 or by_samples) and not subset) else mine,
-                                  max_buffer_bytes=40 << 30, sample_begin=s_begin, sum_only=by_samples)
     # untimed: load the code object, upload the scene, allocate every buffer
-    pt.prepare(ds, params)
+    share.prepare()
     torch.cuda.synchronize()
 
     def step():
         fb.zero_()
-        st = pt.render_device(ds, params, fb.data_ptr(), stream.cuda_stream, stats=True)
+        st = share.render(fb.data_ptr(), stream.cuda_stream)
         if dist is not None:
             dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
-            if by_samples and rank == 0:
-                fb.div_(float(spp))  # the ranks' sample sums, summed, over spp: tracePixel's mean
+            share.finish(fb)  # rank 0, sample split: the ranks' sums over spp
         return st
 
     for _ in range(args.warmup):
@@ -220,7 +227,8 @@ def main():
                 cfg.name, W, H, spp, cfg.depth, cfg.note,
                 ("; timed on %d hashed pixels at full spp" % subset) if subset else ""),
                        "order": args.order,
-                       "sharding": ("one GPU renders every pixel" if world == 1 else
+                       "sharding": (("one GPU renders every pixel" if not subset else
+                                     "one GPU renders %d hashed pixels of the frame" % subset) if world == 1 else
                                     "every pixel, spp split over ranks, per-pixel sums + RCCL reduce" if by_samples
                                     else "16x16 tiles hashed over ranks + RCCL reduce")},
             "samples_per_step": npix_total * spp,
@@ -247,7 +255,7 @@ def main():
                     "salu_insts_per_simd_cycle": round(ev.get("salu_insts_per_simd_cycle", 0), 4),
                     "valu_busy_rocprof": round(ev["valu_busy"], 4),
                     "hbm_GBps": round(ev["hbm_GBps"], 2), "hbm_peak_GBps": 8000.0})
-        if not args.no_cpu and world == 1:
+        if not args.no_cpu:  # rank 0, after the timed region (the other ranks are done)
             try:
                 npx = args.cpu_pixels or CPU_PIXELS.get(cfg.name, 512)
                 pix, ref, cb = cpu_baseline(cfg, to_text(root, "/tmp/pt_bench_img"), spp, npx,

@@ -12,6 +12,9 @@
  *   Object, Sphere, Plane, Union,
  *   Intersection, Difference,
  *   TransformedObject, transform()   include/object.h, sphere.h, plane.h, union.h, ...
+ *   Ray, Span, SpanIterator          include/ray.h, include/span.h:12-171
+ *   Object::makeSpanIterator(),      the query virtuals, served by the device
+ *   Texture::getColor / getFloat     (pt_query_spans / pt_tex_eval)
  *   unionArray                       src/test.cpp:52-64
  *
  * What differs is the last step: instead of world->makeSpanIterator() and a
@@ -283,6 +286,15 @@ private:
     unsigned w_, h_;
 };
 
+/* ------------------------------------------------------------------- Ray -- */
+struct Ray /* include/ray.h:9-23 */
+{
+    Vector3D origin;
+    Vector3D dir;
+    Ray(Vector3D origin, Vector3D dir) : origin(origin), dir(dir) {}
+    Vector3D getPoint(float t) const { return origin + t * dir; }
+};
+
 /* ------------------------------------------------------------- flattening -- */
 class Texture;
 struct Material;
@@ -309,6 +321,33 @@ public:
 
 private:
     std::map<const void *, pt_id> textures_, materials_, images_;
+
+public:
+    /* the Material a flattened material id stands for (span queries) */
+    const Material *material_of(pt_id id) const
+    {
+        for (const auto &kv : materials_)
+            if (kv.second == id)
+                return static_cast<const Material *>(kv.first);
+        return nullptr;
+    }
+};
+
+/* A private pt_scene holding one flattened object or texture: what the
+ * query virtuals evaluate on the device. */
+struct DeviceQueryScene
+{
+    pt_scene *s;
+    Flattener f;
+    pt_id id = -1;
+    DeviceQueryScene() : s(pt_scene_create()), f(s)
+    {
+        if (!s)
+            throw DeviceError(PT_ERR_DEVICE, pt_last_error());
+    }
+    ~DeviceQueryScene() { pt_scene_destroy(s); }
+    DeviceQueryScene(const DeviceQueryScene &) = delete;
+    DeviceQueryScene &operator=(const DeviceQueryScene &) = delete;
 };
 
 /* --------------------------------------------------------------- textures -- */
@@ -316,18 +355,64 @@ class Texture /* include/texture.h:10-27 */
 {
 public:
     virtual ~Texture() {}
+    /* getColor / getFloat (texture.h:13-18).  The built-in classes answer on
+     * the device (pt_tex_eval of this texture, flattened once); a user-defined
+     * subclass overrides getColor as in the reference -- it then works on the
+     * host, but has no device form, so a scene using it cannot be rendered. */
+    virtual Color getColor(Vector3D pos) const
+    {
+        Color c;
+        float v;
+        eval(&pos, 1, &c, &v);
+        return c;
+    }
+    virtual float getFloat(Vector3D pos) const
+    {
+        if (!device_form_) { /* the reference's default: the mean of getColor */
+            Color c = getColor(pos);
+            return (c.x + c.y + c.z) * (1.0f / 3.0f);
+        }
+        Color c;
+        float v;
+        eval(&pos, 1, &c, &v);
+        return v;
+    }
+    /* many lookups in one device call: colors[i], values[i] at pos[i] */
+    void getColors(const Vector3D *pos, size_t n, Color *colors, float *values) const { eval(pos, n, colors, values); }
     virtual Texture *duplicate() const = 0;
     virtual Texture *transform(const Matrix &) const { return nullptr; }
-    virtual pt_id flatten(Flattener &f) const = 0;
+    virtual pt_id flatten(Flattener &) const
+    {
+        throw DeviceError(PT_ERR_ARG, "a user-defined Texture subclass has no device form");
+    }
+
+protected:
+    Texture() = default;
+    explicit Texture(bool device_form) : device_form_(device_form) {}
+
+private:
+    bool device_form_ = false;
+    mutable std::shared_ptr<DeviceQueryScene> q_;
+    void eval(const Vector3D *pos, size_t n, Color *colors, float *values) const
+    {
+        static_assert(sizeof(Vector3D) == 3 * sizeof(float), "Vector3D must be 3 packed floats");
+        if (!q_) {
+            std::shared_ptr<DeviceQueryScene> q(new DeviceQueryScene);
+            q->id = flatten(q->f);
+            q_ = q;
+        }
+        ptCheck(pt_tex_eval(q_->s, q_->id, reinterpret_cast<const float *>(pos), (int64_t)n,
+                            reinterpret_cast<float *>(colors), values, 0));
+    }
 };
 
 class ColorTexture : public Texture /* texture.h:29-58 */
 {
 public:
     Color color;
-    ColorTexture(Color color) : color(color) {}
-    ColorTexture(float r, float g, float b) : color(r, g, b) {}
-    ColorTexture(float v) : color(v) {}
+    ColorTexture(Color color) : Texture(true), color(color) {}
+    ColorTexture(float r, float g, float b) : Texture(true), color(r, g, b) {}
+    ColorTexture(float v) : Texture(true), color(v) {}
     Texture *duplicate() const override { return new ColorTexture(color); }
     Texture *transform(const Matrix &) const override { return new ColorTexture(color); }
     pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_color(f.s, color.x, color.y, color.z)); }
@@ -336,7 +421,7 @@ public:
 class TransformedTexture : public Texture /* texture.h:60-90 */
 {
 public:
-    TransformedTexture(const Matrix &m, Texture *t) : m(m), t(t) {}
+    TransformedTexture(const Matrix &m, Texture *t) : Texture(true), m(m), t(t) {}
     ~TransformedTexture() override { delete t; }
     Texture *duplicate() const override { return new TransformedTexture(m, t->duplicate()); }
     Texture *transform(const Matrix &m2) const override { return new TransformedTexture(m.concat(m2), t->duplicate()); }
@@ -361,7 +446,7 @@ inline Texture *transform(const Matrix &m, Texture *t) /* texture.h:92-98 */
 class ImageTexture : public Texture /* image_texture.h:9-33 */
 {
 public:
-    explicit ImageTexture(Image image) : image(image) {}
+    explicit ImageTexture(Image image) : Texture(true), image(image) {}
     Texture *duplicate() const override { return new ImageTexture(image); }
     pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_image(f.s, f.image(image))); }
     Image image;
@@ -370,7 +455,7 @@ public:
 class ImageAlphaTexture : public Texture /* image_texture.h:35-70 */
 {
 public:
-    explicit ImageAlphaTexture(Image image) : image(image) {}
+    explicit ImageAlphaTexture(Image image) : Texture(true), image(image) {}
     Texture *duplicate() const override { return new ImageAlphaTexture(image); }
     pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_image_alpha(f.s, f.image(image))); }
     Image image;
@@ -380,7 +465,7 @@ class ImageSkyboxTexture : public Texture /* image_texture.h:72-115 */
 {
 public:
     ImageSkyboxTexture(Image top, Image bottom, Image left, Image right, Image front, Image back)
-        : faces{top, bottom, left, right, front, back}
+        : Texture(true), faces{top, bottom, left, right, front, back}
     {
     }
     Texture *duplicate() const override
@@ -400,7 +485,7 @@ class ImageSkyboxAlphaTexture : public Texture /* image_texture.h:117-181 */
 {
 public:
     ImageSkyboxAlphaTexture(Image top, Image bottom, Image left, Image right, Image front, Image back)
-        : faces{top, bottom, left, right, front, back}
+        : Texture(true), faces{top, bottom, left, right, front, back}
     {
     }
     Texture *duplicate() const override
@@ -421,7 +506,7 @@ public:
 class WrapTexture : public Texture
 {
 public:
-    explicit WrapTexture(Texture *t) : t(t) {}
+    explicit WrapTexture(Texture *t) : Texture(true), t(t) {}
     ~WrapTexture() override { delete t; }
 
 protected:
@@ -525,15 +610,115 @@ inline pt_id Flattener::material(const Material *m)
     return materials_[m] = id;
 }
 
+/* ------------------------------------------------------------------- spans -- */
+class Span /* include/span.h:12-120 */
+{
+public:
+    float start = 0;
+    Vector3D startNormal;
+    const Material *startMaterial = nullptr;
+    float end = 0;
+    Vector3D endNormal;
+    const Material *endMaterial = nullptr;
+    Span() = default;
+    Span(float start, Vector3D startNormal, const Material *startMaterial, float end, Vector3D endNormal,
+         const Material *endMaterial)
+        : start(start), startNormal(startNormal), startMaterial(startMaterial), end(end), endNormal(endNormal),
+          endMaterial(endMaterial)
+    {
+    }
+    virtual ~Span() {}
+    bool isEmpty() const { return end <= start; }
+    explicit operator bool() const { return end > start; }
+    bool operator!() const { return end <= start; }
+};
+
+class SpanIterator /* include/span.h:129-171 */
+{
+public:
+    virtual const Span &operator*() const = 0;
+    virtual const Span *operator->() const = 0;
+    virtual bool isAtEnd() const = 0;
+    virtual void next() = 0;
+    virtual void init(const Ray &ray) = 0;
+    virtual ~SpanIterator() {}
+    bool operator!() const { return isAtEnd(); }
+    explicit operator bool() const { return !isAtEnd(); }
+    void operator++(int) { next(); }
+    const SpanIterator &operator++()
+    {
+        next();
+        return *this;
+    }
+
+protected:
+    SpanIterator() = default;
+    SpanIterator(const SpanIterator &) = delete;
+    SpanIterator &operator=(const SpanIterator &) = delete;
+};
+
 /* ----------------------------------------------------------------- objects -- */
 class Object /* include/object.h:10-24 */
 {
 public:
     virtual ~Object() {}
+    /* object.h:14: the object's span iterator.  Built-in objects answer on the
+     * device: init(ray) runs pt_query_spans on this object's flattened copy and
+     * next() walks the returned list (bit-identical to the reference's lazy
+     * iterators, Difference quirk included).  A user-defined subclass
+     * overrides it as in the reference (host-only, not renderable). */
+    inline virtual SpanIterator *makeSpanIterator() const;
     virtual Object *transform(const Matrix &) const { return nullptr; }
     virtual Object *duplicate() const = 0;
-    virtual pt_id flatten(Flattener &f) const = 0;
+    virtual pt_id flatten(Flattener &) const
+    {
+        throw DeviceError(PT_ERR_ARG, "a user-defined Object subclass has no device form");
+    }
 };
+
+/* The device-served SpanIterator of a built-in object (one query per init). */
+class DeviceSpanIterator : public SpanIterator
+{
+public:
+    explicit DeviceSpanIterator(const Object *o) : q_(new DeviceQueryScene)
+    {
+        q_->id = o->flatten(q_->f);
+    }
+    const Span &operator*() const override { return spans_.at(k_); }
+    const Span *operator->() const override { return &spans_.at(k_); }
+    bool isAtEnd() const override { return k_ >= spans_.size(); }
+    void next() override
+    {
+        if (k_ < spans_.size())
+            k_++;
+    }
+    void init(const Ray &ray) override
+    {
+        const float r[6] = {ray.origin.x, ray.origin.y, ray.origin.z, ray.dir.x, ray.dir.y, ray.dir.z};
+        int32_t count = 0;
+        std::vector<pt_span> buf(8);
+        ptCheck(pt_query_spans(q_->s, q_->id, r, 1, (int)buf.size(), buf.data(), &count, 0));
+        if (count > (int32_t)buf.size()) {
+            buf.resize((size_t)count);
+            ptCheck(pt_query_spans(q_->s, q_->id, r, 1, count, buf.data(), &count, 0));
+        }
+        spans_.clear();
+        for (int32_t i = 0; i < count; i++) {
+            const pt_span &p = buf[(size_t)i];
+            spans_.push_back(Span(p.t_start, Vector3D(p.n_start[0], p.n_start[1], p.n_start[2]),
+                                  q_->f.material_of(p.mat_start), p.t_end,
+                                  Vector3D(p.n_end[0], p.n_end[1], p.n_end[2]), q_->f.material_of(p.mat_end)));
+        }
+        k_ = 0;
+    }
+
+private:
+    std::unique_ptr<DeviceQueryScene> q_;
+    std::vector<Span> spans_;
+    size_t k_ = 0;
+};
+
+inline SpanIterator *Object::makeSpanIterator() const { return new DeviceSpanIterator(this); }
 
 class TransformedObject : public Object /* object.h:26-98 */
 {

@@ -219,6 +219,33 @@ int pt_scene_set_fast_spine(pt_scene *s, int on);
 /* Key of the code object for this scene/depth (hex string, static storage). */
 const char *pt_scene_kernel_key(pt_scene *s, int depth);
 
+/* ------------------------------------------------------------ queries --- */
+/* The reference's query virtuals, evaluated on the device.
+ *
+ * pt_query_spans: obj->makeSpanIterator() (include/object.h:14), then for each
+ * ray (6 floats: origin xyz, direction xyz) init(ray) and next() until
+ * isAtEnd() (include/span.h:129-171).  counts[i] receives ray i's number of
+ * spans; the first min(counts[i], max_spans) spans go to out[i * max_spans ..]
+ * in the reference's Span form (span.h:12-120; materials as pt_ids).  obj < 0
+ * queries the scene root.  The lists are bit-identical to the reference's,
+ * including the Difference quirk (src/difference.cpp:124-130). */
+typedef struct pt_span {
+    float t_start, n_start[3];     /* start, startNormal   */
+    int32_t mat_start;             /* startMaterial        */
+    float t_end, n_end[3];         /* end, endNormal       */
+    int32_t mat_end;               /* endMaterial          */
+} pt_span;
+int pt_query_spans(pt_scene *s, pt_id obj, const float *rays, int64_t n, int max_spans, pt_span *out,
+                   int32_t *counts, int device);
+/* Texture::getColor (rgb: 3 floats per point) and Texture::getFloat (value: 1
+ * float per point) of texture tex at n points (3 floats each),
+ * include/texture.h:13-18 with every subclass's override. */
+int pt_tex_eval(pt_scene *s, pt_id tex, const float *points, int64_t n, float *rgb, float *value, int device);
+/* Compile (or fetch from the code-object cache) the query module of obj
+ * (-1: the root, when tex < 0; -2: none) and/or tex (-1: none), without a
+ * device. */
+int pt_query_compile(pt_scene *s, pt_id obj, pt_id tex);
+
 /* Device self-test: the megakernel's exact fast paths for f32 sqrt / '/' /
  * normalize against the compiler's correctly rounded ones on n hashed inputs.
  * mismatches[0..2] receive the sqrt, div and normalize mismatch counts. */

@@ -1330,6 +1330,30 @@ int oracle_spans(const char *scene_text, const float *rays, int n, char *out, in
     }
 }
 
+/* Texture::getColor / getFloat of every texture of the scene text (in file
+ * order) at n points; layout as ptref's "tex" mode: per texture, per point,
+ * r g b value (float32). */
+int oracle_tex_eval(const char *scene_text, const float *pts, int n, float *out)
+{
+    try {
+        scenetext::Desc d = scenetext::parse(scene_text);
+        std::unique_ptr<Scene> scene = load_scene(scene_text);
+        size_t o = 0;
+        for (const scenetext::Item &t : d.textures) {
+            std::unique_ptr<Tex> tex = make_tex(d, *scene, t.id);
+            for (int k = 0; k < n; k++) {
+                const V3 p(pts[3 * k], pts[3 * k + 1], pts[3 * k + 2]);
+                const V3 c = tex->color(p);
+                out[o++] = c.x, out[o++] = c.y, out[o++] = c.z, out[o++] = tex->value(p);
+            }
+        }
+        return 0;
+    } catch (std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 /* Vector-math known answers in the exact layout of ptref's "kat" mode, so the
  * two can be compared word for word. */
 int oracle_kat(uint32_t *out, int64_t cap, int64_t *written)

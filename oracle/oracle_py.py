@@ -21,7 +21,7 @@ LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "ptref")
 
 ORDER_REFERENCE = 0
-ORDER_GROUP64 = 1
+ORDER_FAST = 1
 
 STAT_NAMES = ["queries", "sphere_tests", "sphere_hits", "plane_tests", "merge_steps", "shaded",
               "refract_children", "scatter_children", "attempts", "draws", "leaf_children"]
@@ -51,6 +51,8 @@ def lib():
         L.oracle_spans.restype = ctypes.c_int
         L.oracle_spans.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                    ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+        L.oracle_tex_eval.restype = ctypes.c_int
+        L.oracle_tex_eval.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         C = ctypes
         L.oracle_render_gw.restype = C.c_int
         L.oracle_render_gw.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
@@ -193,6 +195,34 @@ def ref_render(scene_text: str, W: int, H: int, spp: int, depth: int, screen=Non
     if info:
         return res, json.loads(out.strip().splitlines()[-1])
     return res
+
+
+def tex_eval(scene_text: str, points: np.ndarray):
+    """getColor / getFloat of every texture of the scene (file order) at each
+    point: (ntex, npts, 4) float32 r g b value."""
+    import re
+    pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+    ntex = len(re.findall(r"^tex ", scene_text, flags=re.M))
+    out = np.zeros((ntex, len(pts), 4), dtype=np.float32)
+    if lib().oracle_tex_eval(scene_text.encode(), pts.ctypes.data, len(pts), out.ctypes.data) != 0:
+        raise RuntimeError("oracle_tex_eval: " + lib().oracle_last_error().decode())
+    return out
+
+
+def ref_tex_eval(scene_text: str, points: np.ndarray):
+    """The same from the unmodified reference (ptref "tex" mode)."""
+    import re
+    pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+    ntex = len(re.findall(r"^tex ", scene_text, flags=re.M))
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "scene.txt")
+        with open(sp, "w") as f:
+            f.write(scene_text)
+        pp = os.path.join(td, "pts.bin")
+        pts.tofile(pp)
+        op = os.path.join(td, "out.bin")
+        _ref(["tex", sp, pp, op])
+        return np.fromfile(op, dtype=np.float32).reshape(ntex, len(pts), 4)
 
 
 def ref_spans(scene_text: str, rays: np.ndarray):

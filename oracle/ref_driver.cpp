@@ -19,6 +19,7 @@
  * Modes (argv[1]):
  *   render  scene.txt W H spp depth sw sh dist seed pixels.bin|all threads per_sample out.bin
  *   spans   scene.txt rays.bin out.bin       full span list of root for each ray
+ *   tex     scene.txt points.bin out.bin     getColor / getFloat of every texture at each point
  *   kat     out.bin                          engine / math known-answer vectors
  *   hdr     in.hdr out_rgba.bin out_rewritten.hdr   reference HDR read + writeHDR
  *   writehdr w h rgba.bin out.hdr            reference MutableImage::writeHDR
@@ -392,6 +393,35 @@ int mode_writehdr(int argc, char **argv)
     return 0;
 }
 
+/* tex: Texture::getColor and Texture::getFloat (include/texture.h:13-18, through
+ * the virtuals, so every subclass's override) of each texture of the scene
+ * text, in file order, at every point of points.bin (3 float32 each); out.bin =
+ * per texture, per point, r g b value (float32). */
+int mode_tex(int argc, char **argv)
+{
+    if (argc != 5)
+        return 2;
+    std::vector<char> txt = read_file(argv[2]);
+    scenetext::Desc d = scenetext::parse(std::string(txt.data(), txt.size()));
+    World w;
+    build_world(d, w);
+    std::vector<char> raw = read_file(argv[3]);
+    const float *p = (const float *)raw.data();
+    const size_t n = raw.size() / 12;
+    std::vector<float> out;
+    for (const scenetext::Item &t : d.textures) {
+        Texture *tex = build_tex(d, w, t.id);
+        for (size_t k = 0; k < n; k++) {
+            const Vector3D v(p[3 * k], p[3 * k + 1], p[3 * k + 2]);
+            const Color c = tex->getColor(v);
+            out.push_back(c.x), out.push_back(c.y), out.push_back(c.z), out.push_back(tex->getFloat(v));
+        }
+        delete tex;
+    }
+    write_file(argv[4], out.data(), out.size() * 4);
+    return 0;
+}
+
 /* matrix: in.bin = n records of {float axis[3]; float pad; double angle; float m[12]; float m2[12]},
  * out.bin = n records of {rotate(axis, angle)[12], invert(m)[12] (NaN if singular), m.concat(m2)[12]}. */
 int mode_matrix(int argc, char **argv)
@@ -449,6 +479,8 @@ int main(int argc, char **argv)
             return mode_writehdr(argc, argv);
         if (m == "matrix")
             return mode_matrix(argc, argv);
+        if (m == "tex")
+            return mode_tex(argc, argv);
         fprintf(stderr, "unknown mode %s\n", m.c_str());
         return 2;
     } catch (std::exception &e) {

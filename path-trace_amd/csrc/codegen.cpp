@@ -316,6 +316,37 @@ Generated generate(const SceneImpl &s, int depth)
     out.n_spheres = g.spheres;
     out.n_planes = g.planes;
     out.n_mats = (int)g.mats.size();
+    out.mat_ids = g.mats;
+    char key[40];
+    snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(out.source));
+    out.key = key;
+    return out;
+}
+
+Generated generate_query(const SceneImpl &s, int obj, int tex)
+{
+    Gen g(s);
+    std::ostringstream src;
+    src << device_library_source() << "\n";
+    src << "namespace ptgen {\nusing namespace ptd;\n";
+    if (obj >= 0)
+        src << "typedef " << g.obj(obj) << " QRoot;\n";
+    if (tex >= 0)
+        src << "typedef " << g.tex(tex) << " QTex;\n";
+    src << "} // namespace ptgen\n";
+    if (obj >= 0)
+        src << "PT_DEFINE_QUERY(ptgen::QRoot)\n";
+    if (tex >= 0)
+        src << "PT_DEFINE_TEXEVAL(ptgen::QTex)\n";
+    Generated out;
+    out.source = src.str();
+    out.params = std::move(g.P);
+    if (out.params.empty())
+        out.params.push_back(0.0f);
+    out.image_ids = g.images;
+    out.n_prims = g.prim;
+    out.n_mats = (int)g.mats.size();
+    out.mat_ids = g.mats;
     char key[40];
     snprintf(key, sizeof key, "%016llx", (unsigned long long)fnv1a(out.source));
     out.key = key;

@@ -348,9 +348,13 @@ __device__ __forceinline__ int mbcnt(u64 m, int base)
 {
     return (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, (u32)base));
 }
-/* this lane's bit of the uniform mask m (the JIT runs on the clang that torch
- * bundles, which has no __builtin_amdgcn_inverse_ballot_w64) */
+/* this lane's bit of the uniform mask m, by arithmetic */
 __device__ __forceinline__ bool lane_in(u64 m) { return (m >> (threadIdx.x & 63)) & 1ull; }
+/* the same as a branch condition: `if (in_mask(m))` runs the block with exec = m
+ * (s_and_saveexec on the mask itself, no per-lane compare).  The LLVM intrinsic
+ * is named directly: the hiprtc front end lacks its clang builtin. */
+extern "C" __device__ bool pt_llvm_inverse_ballot(u64) __asm("llvm.amdgcn.inverse.ballot.i64");
+__device__ __forceinline__ bool in_mask(u64 m) { return pt_llvm_inverse_ballot(m); }
 __device__ __forceinline__ int nth_set_bit(u64 m, int k) /* 1-based k, m has >= k bits */
 {
     for (int j = 1; j < k; j++)
@@ -1892,12 +1896,22 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 #endif
             int ta = 0, tk = 0; /* accepted / kept attempts of the round */
             u64 nlor = 0ull, Alast = 0ull, Flast = 0ull;
-            /* one attempt's ring entry (kept, with a free slot) */
-            auto write_attempt = [&](u64 A, u64 kp, V3 wn, float factor) {
-                const int kl = lane_bit(kp);
-                const int ko = mbcnt(kp, tk);
-                if (kl && ko < free_slots)
-                    ring[(nkeep + ko) & (PT_RCAP - 1)] = make_float4(wn.x, wn.y, wn.z, factor);
+            /* One attempt's ring entry (kept, with a free slot).  A deferred
+             * burst parks the attempt's engine state (8 bytes, one register
+             * pair): the first pass draws its three numbers again, which costs
+             * less there -- 64 kept children per wave instruction -- than
+             * moving the direction into a 16-byte store here, where a wave
+             * instruction covers 64 attempts of which few are kept.  The
+             * store runs under exec = kept mask & slot available. */
+            const int slot_end = nkeep + free_slots;
+            auto write_attempt = [&](u64 A, u64 kp, u64 st, V3 wn, float factor) {
+                const int slot = mbcnt(kp, nkeep + tk);
+                if (in_mask(kp & __ballot(slot < slot_end))) {
+                    if (DEFERRED)
+                        __builtin_memcpy(&ring[slot & (PT_RCAP - 1)], &st, 8);
+                    else
+                        ring[slot & (PT_RCAP - 1)] = make_float4(wn.x, wn.y, wn.z, factor);
+                }
                 ta += __popcll(A);
                 tk += __popcll(kp);
             };
@@ -1910,17 +1924,17 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         sk = A64 * sk + g64inc;
                     const u64 sk1 = A64 * sk + g64inc;
                     const Attempt2 ap = attempt2<KR0>(sk, sk1, n, kR);
-                    sk = sk1;
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
                         u64 D = 0ull;
                         if (RAW)
                             D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
-                        write_attempt(ap.A[h], ap.A[h] & ~D, wn, 0.0f);
+                        write_attempt(ap.A[h], ap.A[h] & ~D, h ? sk1 : sk, wn, 0.0f);
                         if (k + h == PT_KATT - 1)
                             Alast = ap.A[h], Flast = ap.F[h];
                     }
+                    sk = sk1;
                 }
             } else {
                 u64 sk = A3l * rng.st + ginc;
@@ -1929,7 +1943,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     if (k)
                         sk = A64 * sk + g64inc;
                     const Attempt at = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
-                    write_attempt(at.A, at.A, at.wn, at.factor);
+                    write_attempt(at.A, at.A, sk, at.wn, at.factor);
                     nlor |= at.NL;
                     if (k == PT_KATT - 1)
                         Alast = at.A, Flast = at.F;
@@ -2166,9 +2180,17 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 if (lane < cf) {
                     float4 en = ring[pos & (PT_RCAP - 1)];
                     if (DEFERRED) {
-                        /* the normalisation and factor of path-trace.h:157, :160,
+                        /* the parked attempt's three draws again (attempt2's
+                         * arithmetic element by element: the same w), then the
+                         * normalisation and factor of path-trace.h:157, :160,
                          * left to this pass so that 64 useful lanes do them */
-                        const V3 nd = cnormalize(mk(en.x, en.y, en.z));
+                        u64 st;
+                        __builtin_memcpy(&st, &en, 8);
+                        const W2 s1 = lcg_step({(u32)st, (u32)(st >> 32)}), s2 = lcg_step(s1), s3 = lcg_step(s2);
+                        V3 w = mk(u11(s1.hi), u11(s2.hi), u11(s3.hi));
+                        if (!KR0)
+                            w = w + kR;
+                        const V3 nd = cnormalize(w);
                         en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
                     }
                     if constexpr (CLEAR) {
@@ -2743,10 +2765,82 @@ __device__ constexpr int min_workgroups()
     return n < 1 ? 1 : n > 5 ? 5 : n;
 }
 
+/* ---- boundary queries (pt_query_spans, pt_tex_eval) -------------------
+ * The reference's query virtuals served on the device, one ray / point per
+ * lane.  SpanIterator (include/span.h:129-171) of an object: init(ray), then
+ * next() until isAtEnd(); every span in the reference's Span form (start,
+ * startNormal, startMaterial, end, endNormal, endMaterial; span.h:12-120) --
+ * the same lazy merges the render kernel runs, with each normal recomputed
+ * from (ray, t, primitive, flip) as the render kernel does for its hit
+ * (copyEndFromStart / copyStartFromEnd negate, span.h:100-112).  Ten words per
+ * span: t, normal, material (compact index, as int bits) for each end. */
+template <class R>
+__device__ __forceinline__ void query_spans(const Env &e, const float *__restrict__ rays, long long n, int max_spans,
+                                            float *__restrict__ out, int *__restrict__ counts)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const float *r = rays + 6 * i;
+    const V3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
+    typename R::Ctx ctx;
+    R::prep_l(ctx, o, e);
+    typename R::St st;
+    R::init(st, ctx, mkray(d), e);
+    CS sp;
+    int c = 0;
+    while (R::pull(st, sp)) {
+        if (c < max_spans) {
+            V3 n0 = R::normal(ref_prim(sp.r0), sp.t0, o, d, e), n1 = R::normal(ref_prim(sp.r1), sp.t1, o, d, e);
+            if (sp.r0 & FLIP)
+                n0 = -n0;
+            if (sp.r1 & FLIP)
+                n1 = -n1;
+            float *q = out + ((long long)i * max_spans + c) * 10;
+            q[0] = sp.t0, q[1] = n0.x, q[2] = n0.y, q[3] = n0.z, q[4] = __int_as_float(ref_mat(sp.r0));
+            q[5] = sp.t1, q[6] = n1.x, q[7] = n1.y, q[8] = n1.z, q[9] = __int_as_float(ref_mat(sp.r1));
+        }
+        c++;
+    }
+    counts[i] = c;
+}
+/* Texture::getColor / getFloat (include/texture.h:13-18) at one point per lane */
+template <class T>
+__device__ __forceinline__ void tex_eval(const Env &e, const float *__restrict__ pts, long long n,
+                                         float *__restrict__ rgb, float *__restrict__ val)
+{
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const V3 p = mk(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+    const V3 c = T::color(p, e);
+    rgb[3 * i] = c.x, rgb[3 * i + 1] = c.y, rgb[3 * i + 2] = c.z;
+    val[i] = T::value(p, e);
+}
+
 } // namespace ptd
 
-#ifdef PT_MIN_WAVES /* experiment override */
-#define PT_MIN_WG(SCENE, MAXD) PT_MIN_WAVES
+#define PT_DEFINE_QUERY(ROOT)                                                                               \
+    extern "C" __global__ __launch_bounds__(256) void pt_query_spans(                                      \
+        const float *__restrict__ P, const ptd::PtImage *__restrict__ imgs, const float *__restrict__ rays, \
+        long long n, int max_spans, float *__restrict__ out, int *__restrict__ counts)                    \
+    {                                                                                                       \
+        const ptd::Env e = {P, imgs};                                                                       \
+        ptd::query_spans<ROOT>(e, rays, n, max_spans, out, counts);                                         \
+    }
+#define PT_DEFINE_TEXEVAL(TEX)                                                                              \
+    extern "C" __global__ __launch_bounds__(256) void pt_tex_eval(                                         \
+        const float *__restrict__ P, const ptd::PtImage *__restrict__ imgs, const float *__restrict__ pts,  \
+        long long n, float *__restrict__ rgb, float *__restrict__ val)                                     \
+    {                                                                                                       \
+        const ptd::Env e = {P, imgs};                                                                       \
+        ptd::tex_eval<TEX>(e, pts, n, rgb, val);                                                            \
+    }
+
+#ifdef PT_MIN_WAVES /* per scene (pt_scene_set_occupancy), never above what LDS admits: a higher
+                       cap would only lower the VGPR budget without adding a resident wave */
+#define PT_MIN_WG(SCENE, MAXD)                                                                              \
+    (PT_MIN_WAVES < ptd::min_workgroups<SCENE, MAXD>() ? PT_MIN_WAVES : ptd::min_workgroups<SCENE, MAXD>())
 #else
 #define PT_MIN_WG(SCENE, MAXD) (ptd::min_workgroups<SCENE, MAXD>())
 #endif

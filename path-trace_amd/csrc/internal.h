@@ -86,11 +86,15 @@ struct Generated
     std::string key;            /* content hash of source + options + compiler        */
     std::vector<float> params;  /* scene parameter block P                           */
     std::vector<int> image_ids; /* slot -> scene image index                          */
+    std::vector<int> mat_ids;   /* compact material index -> scene material index     */
     int maxd = 0;
     int n_prims = 0, n_spheres = 0, n_planes = 0, n_mats = 0;
 };
 
 Generated generate(const SceneImpl &s, int depth);
+/* Query module for the boundary's query virtuals: pt_query_spans over object
+ * `obj` (if >= 0) and pt_tex_eval of texture `tex` (if >= 0). */
+Generated generate_query(const SceneImpl &s, int obj, int tex);
 /* Returns the gfx950 code object for g (from the cache or compiled now). */
 const std::vector<char> &code_object(const Generated &g);
 

@@ -719,6 +719,59 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
     }
 }
 
+/* A query module (generate_query) loaded on one device with its own copy of
+ * the parameters and images; everything is released with it. */
+struct QueryModule
+{
+    int device;
+    hipModule_t mod = nullptr;
+    DevBuf<float> P;
+    DevBuf<PtImageDev> imgs;
+    std::vector<DevBuf<float>> img_data;
+    std::vector<void *> scratch;
+    QueryModule(SceneImpl &s, const Generated &g, int dev) : device(dev)
+    {
+        const std::vector<char> &code = code_object(g);
+        HIPCHECK(hipSetDevice(device));
+        HIPCHECK(hipModuleLoadData(&mod, code.data()));
+        P.ensure(g.params.size());
+        HIPCHECK(hipMemcpy(P.p, g.params.data(), g.params.size() * 4, hipMemcpyHostToDevice));
+        img_data.resize(g.image_ids.size());
+        std::vector<PtImageDev> desc(g.image_ids.size() + 1);
+        for (size_t k = 0; k < g.image_ids.size(); k++) {
+            const ImageRec &im = s.images.at(g.image_ids[k]);
+            img_data[k].ensure(im.rgba.size());
+            HIPCHECK(hipMemcpy(img_data[k].p, im.rgba.data(), im.rgba.size() * 4, hipMemcpyHostToDevice));
+            desc[k].data = img_data[k].p;
+            desc[k].w = (uint32_t)im.w;
+            desc[k].h = (uint32_t)im.h;
+        }
+        imgs.ensure(desc.size());
+        HIPCHECK(hipMemcpy(imgs.p, desc.data(), desc.size() * sizeof(PtImageDev), hipMemcpyHostToDevice));
+    }
+    void *alloc(size_t bytes)
+    {
+        void *q = nullptr;
+        HIPCHECK(hipMalloc(&q, bytes ? bytes : 4));
+        scratch.push_back(q);
+        return q;
+    }
+    hipFunction_t fn(const char *name)
+    {
+        hipFunction_t f;
+        HIPCHECK(hipModuleGetFunction(&f, mod, name));
+        return f;
+    }
+    ~QueryModule()
+    {
+        for (void *q : scratch) (void)hipFree(q);
+        P.release(), imgs.release();
+        for (auto &b : img_data) b.release();
+        if (mod)
+            (void)hipModuleUnload(mod);
+    }
+};
+
 } // namespace
 
 } // namespace pt
@@ -1169,6 +1222,8 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
             throw Error(PT_ERR_ARG, "null output or adaptive params");
         if (p->pixels)
             throw Error(PT_ERR_ARG, "adaptive render takes no pixel list");
+        if (p->sum_only)
+            throw Error(PT_ERR_ARG, "adaptive render interpolates means: sum_only is not supported");
         validate(p);
         (void)S(s);
         const int W = p->width, H = p->height;
@@ -1236,7 +1291,8 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
             acc.kernel_ms += st.kernel_ms, acc.reduce_ms += st.reduce_ms, acc.launches += st.launches;
             acc.samples += st.samples, acc.queries += st.queries, acc.leaf_queries += st.leaf_queries;
             acc.attempts += st.attempts, acc.rounds += st.rounds, acc.slow_queries += st.slow_queries;
-            acc.dark_queries += st.dark_queries;
+            acc.dark_queries += st.dark_queries, acc.mid_queries += st.mid_queries;
+            acc.wave_ms += st.wave_ms; /* summed over the batches, like kernel_ms */
             ap->levels++;
             need.clear();
         };
@@ -1345,6 +1401,93 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
                     }
         if (stats)
             *stats = acc;
+        return PT_OK;
+    });
+}
+
+int pt_query_spans(pt_scene *s, pt_id obj, const float *rays, int64_t n, int max_spans, pt_span *out,
+                   int32_t *counts, int device)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        if (obj < 0)
+            obj = sc.root;
+        check_obj(sc, obj);
+        if (n < 0 || max_spans < 0 || (n > 0 && (!rays || !counts || (max_spans > 0 && !out))))
+            throw Error(PT_ERR_ARG, "bad query arguments");
+        if (n == 0)
+            return PT_OK;
+        static_assert(sizeof(pt_span) == 40, "pt_span is ten 4-byte words");
+        Generated g = generate_query(sc, obj, -1);
+        QueryModule q(sc, g, device);
+        float *dr = (float *)q.alloc((size_t)n * 24);
+        float *dout = (float *)q.alloc((size_t)n * std::max(1, max_spans) * 40);
+        int *dc = (int *)q.alloc((size_t)n * 4);
+        HIPCHECK(hipMemcpy(dr, rays, (size_t)n * 24, hipMemcpyHostToDevice));
+        const float *Pp = q.P.p;
+        const PtImageDev *ip = q.imgs.p;
+        long long nn = n;
+        int ms = max_spans;
+        void *args[] = {&Pp, &ip, &dr, &nn, &ms, &dout, &dc};
+        HIPCHECK(hipModuleLaunchKernel(q.fn("pt_query_spans"), (unsigned)((n + 255) / 256), 1, 1, 256, 1, 1, 0,
+                                       nullptr, args, nullptr));
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipMemcpy(counts, dc, (size_t)n * 4, hipMemcpyDeviceToHost));
+        if (max_spans > 0) {
+            HIPCHECK(hipMemcpy(out, dout, (size_t)n * max_spans * 40, hipMemcpyDeviceToHost));
+            /* compact material indices -> the scene's material ids */
+            for (int64_t i = 0; i < n; i++)
+                for (int c = 0; c < std::min<int>(counts[i], max_spans); c++) {
+                    pt_span &sp = out[i * max_spans + c];
+                    sp.mat_start = g.mat_ids.at((size_t)sp.mat_start);
+                    sp.mat_end = g.mat_ids.at((size_t)sp.mat_end);
+                }
+        }
+        return PT_OK;
+    });
+}
+
+int pt_tex_eval(pt_scene *s, pt_id tex, const float *points, int64_t n, float *rgb, float *value, int device)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        check_tex(sc, tex);
+        if (n < 0 || (n > 0 && (!points || !rgb || !value)))
+            throw Error(PT_ERR_ARG, "bad texture query arguments");
+        if (n == 0)
+            return PT_OK;
+        Generated g = generate_query(sc, -1, tex);
+        QueryModule q(sc, g, device);
+        float *dp = (float *)q.alloc((size_t)n * 12), *dc = (float *)q.alloc((size_t)n * 12);
+        float *dv = (float *)q.alloc((size_t)n * 4);
+        HIPCHECK(hipMemcpy(dp, points, (size_t)n * 12, hipMemcpyHostToDevice));
+        const float *Pp = q.P.p;
+        const PtImageDev *ip = q.imgs.p;
+        long long nn = n;
+        void *args[] = {&Pp, &ip, &dp, &nn, &dc, &dv};
+        HIPCHECK(hipModuleLaunchKernel(q.fn("pt_tex_eval"), (unsigned)((n + 255) / 256), 1, 1, 256, 1, 1, 0, nullptr,
+                                       args, nullptr));
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipMemcpy(rgb, dc, (size_t)n * 12, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(value, dv, (size_t)n * 4, hipMemcpyDeviceToHost));
+        return PT_OK;
+    });
+}
+
+/* Compile (or fetch from the cache) the query module of pt_query_spans /
+ * pt_tex_eval without a device. */
+int pt_query_compile(pt_scene *s, pt_id obj, pt_id tex)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        if (obj >= 0)
+            check_obj(sc, obj);
+        if (tex >= 0)
+            check_tex(sc, tex);
+        /* obj -1: the root (unless only a texture is asked for); obj -2: no object */
+        if (obj == -1 && tex < 0)
+            obj = sc.root, check_obj(sc, obj);
+        (void)code_object(generate_query(sc, obj < 0 ? -1 : obj, tex));
         return PT_OK;
     });
 }

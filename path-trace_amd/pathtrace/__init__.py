@@ -50,6 +50,19 @@ class DeviceScene:
         self.root = root
         _lib.check(L.pt_set_root(self._h, self._obj(root)))
 
+    @classmethod
+    def from_text(cls, text: str) -> "DeviceScene":
+        """A pt_scene loaded from the plain-text scene format (pt_scene_from_text);
+        its textures / materials / objects get ids in file order."""
+        self = cls.__new__(cls)
+        L = _lib.lib()
+        self._h = L.pt_scene_create()
+        if not self._h:
+            raise PtError("pt_scene_create failed")
+        self._img, self._mat, self.root = {}, {}, None
+        _lib.check(L.pt_scene_from_text(self._h, text.encode()))
+        return self
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h:
@@ -119,6 +132,39 @@ class DeviceScene:
             ch = self._obj(o.o)
             return c(L.pt_transformed(h, _lib._f12(o.matrix.m), ch))
         raise TypeError("unsupported object %r" % (o,))
+
+    def query_spans(self, rays, max_spans: int = 16, device: int = 0):
+        """obj->makeSpanIterator() over the root for each ray (n x 6: origin,
+        direction), evaluated on the device (pt_query_spans): returns
+        (counts[n], spans[n, max_spans, 10] as float32 words: t, normal,
+        material id (int32 bits) for the start, then for the end)."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        n = len(rays)
+        out = np.zeros((n, max_spans, 10), dtype=np.float32)
+        counts = np.zeros(n, dtype=np.int32)
+        _lib.check(_lib.lib().pt_query_spans(self._h, -1, rays.ctypes.data, n, int(max_spans), out.ctypes.data,
+                                             counts.ctypes.data, int(device)))
+        return counts, out
+
+    def tex_eval(self, texture, points, device: int = 0):
+        """Texture::getColor / getFloat at n points (n x 3) on the device
+        (pt_tex_eval) of a Texture (flattened into this scene) or a texture id:
+        returns (rgb[n, 3], value[n])."""
+        pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+        rgb = np.zeros((len(pts), 3), dtype=np.float32)
+        val = np.zeros(len(pts), dtype=np.float32)
+        tid = int(texture) if isinstance(texture, (int, np.integer)) else self._tex(texture)
+        _lib.check(_lib.lib().pt_tex_eval(self._h, tid, pts.ctypes.data, len(pts), rgb.ctypes.data,
+                                          val.ctypes.data, int(device)))
+        return rgb, val
+
+    def compile_queries(self, textures=()) -> None:
+        """Compile the query modules -- the root's span query and each texture's
+        (Texture objects or ids) -- without a device."""
+        _lib.check(_lib.lib().pt_query_compile(self._h, -1, -1))
+        for t in textures:
+            tid = int(t) if isinstance(t, (int, np.integer)) else self._tex(t)
+            _lib.check(_lib.lib().pt_query_compile(self._h, -2, tid))
 
     def compile(self, depth: int) -> str:
         _lib.check(_lib.lib().pt_scene_compile(self._h, depth))

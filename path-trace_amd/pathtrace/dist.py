@@ -47,3 +47,52 @@ def reduce_frame(fb, group=None):
     import torch.distributed as dist
     dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM, group=group)
     return fb
+
+
+class RankFrame:
+    """One rank's share of a frame, as bench.py renders it (the per-rank step
+    of the multi-GPU run; tests/test_dist_gpu.py drives the same object).
+
+    split "samples": the rank renders every pixel (or `subset`) for samples
+    [r*spp/N, (r+1)*spp/N) and writes per-pixel sums (sample_begin / sum_only);
+    after the sum-reduce rank 0 divides by spp -- tracePixel's mean with the
+    ranks' partial sums added in rank order.  split "tiles": the rank renders
+    the hashed 16x16 tiles it owns (means); the disjoint frames sum-reduce to
+    the single-GPU frame bit for bit.  One rank is the plain full render."""
+
+    def __init__(self, ds, width, height, spp, depth, rank=0, world=1, split="samples", screen=None,
+                 subset=None, order="fast", device=0, max_buffer_bytes=0, seed=0x5EED):
+        from . import make_params
+        if split not in ("samples", "tiles"):
+            raise ValueError("split must be 'samples' or 'tiles'")
+        self.ds, self.rank, self.world, self.spp = ds, rank, world, spp
+        self.by_samples = world > 1 and split == "samples"
+        mine = rank_pixels(width, height, rank, 1 if self.by_samples else world)
+        if subset is not None:
+            mine = np.intersect1d(mine, np.asarray(subset)).astype(np.int32)
+        self.pixels = mine
+        if self.by_samples:
+            self.sample_begin = rank * spp // world
+            self.sample_count = (rank + 1) * spp // world - self.sample_begin
+        else:
+            self.sample_begin, self.sample_count = 0, spp
+        full = (world == 1 or self.by_samples) and subset is None
+        self.params, self._keep = make_params(width, height, self.sample_count, depth, screen=screen, seed=seed,
+                                              order=order, device=device, pixels=None if full else mine,
+                                              max_buffer_bytes=max_buffer_bytes, sample_begin=self.sample_begin,
+                                              sum_only=self.by_samples)
+
+    def prepare(self):
+        from . import prepare
+        prepare(self.ds, self.params)
+
+    def render(self, fb_ptr, stream_ptr=0, stats=True):
+        """this rank's contribution into the zeroed device frame at fb_ptr"""
+        from . import render_device
+        return render_device(self.ds, self.params, fb_ptr, stream_ptr, stats=stats)
+
+    def finish(self, fb):
+        """after the sum-reduce to rank 0: the frame of means (torch tensor, in place)"""
+        if self.by_samples and self.rank == 0:
+            fb.div_(float(self.spp))
+        return fb

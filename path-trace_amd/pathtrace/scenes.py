@@ -202,7 +202,7 @@ CONFIGS: Dict[str, Config] = {
     "C1": Config("C1", 256, 256, 16, 4, scene_p0, note="plumbing; CPU reference path"),
     "C2": Config("C2", 1280, 720, 256, 16, scene_c2, note="8 spheres + plane + mirror-ball env (test2.hdr)"),
     "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG"),
-    "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene, tiles over 8 GPUs + RCCL reduce"),
+    "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene over 8 GPUs + RCCL framebuffer reduce"),
     # C5 at 2 workgroups per CU: its 14-primitive tree spills 1032 VGPRs at the
     # default cap of 128 and its time is spine walks through the glass ball:
     # 119 -> 277 Msamples/s on one MI355X

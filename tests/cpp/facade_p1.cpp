@@ -4,14 +4,44 @@
 //   facade_p1 key DEPTH                 -> prints the scene's code-object key (no GPU)
 //   facade_p1 render W H SPP DEPTH OUT  -> renders on device 0, writes W*H*3 f32 to OUT
 //   facade_p1 errors                    -> checks the error mapping (no GPU)
+//   facade_p1 spans RAYS OUT            -> world->makeSpanIterator() over each ray of RAYS
+//                                          (n x 6 f32): per ray a count, then per span
+//                                          t0 n0 m0 t1 n1 m1 (m = material index below)
+//   facade_p1 tex HDR PTS OUT           -> getColor / getFloat of MirrorBall(Image(HDR))
+//                                          and of a user-defined Texture at each point
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <memory>
+#include <vector>
 
 #include "pt/PathTrace.hpp"
 
 using namespace PathTrace;
+
+/* a reference-style user texture: overrides getColor only (texture.h:13) */
+class Checker : public Texture
+{
+public:
+    Color getColor(Vector3D p) const override
+    {
+        return ((int)std::floor(p.x) + (int)std::floor(p.y) + (int)std::floor(p.z)) % 2 ? Color(1) : Color(0.25f);
+    }
+    Texture *duplicate() const override { return new Checker; }
+};
+
+static std::vector<float> read_f32(const char *path)
+{
+    std::vector<float> v;
+    FILE *f = fopen(path, "rb");
+    if (!f)
+        return v;
+    float x;
+    while (fread(&x, 4, 1, f) == 1) v.push_back(x);
+    fclose(f);
+    return v;
+}
 
 int main(int argc, char **argv)
 {
@@ -51,6 +81,66 @@ int main(int argc, char **argv)
             Matrix r = Matrix::rotateY(0.5);
             Matrix id = r.concat(invert(r));
             printf("errors ok %.6f %.6f\n", id.x00, id.x11);
+            return 0;
+        }
+        if (!strcmp(argv[1], "spans") && argc == 4) {
+            const Material *mats[4] = {&diffuse, &mirror, &glass, &sky};
+            auto mi = [&](const Material *m) {
+                for (int k = 0; k < 4; k++)
+                    if (mats[k] == m)
+                        return k;
+                return -1;
+            };
+            std::vector<float> rays = read_f32(argv[2]);
+            std::unique_ptr<SpanIterator> it(world->makeSpanIterator());
+            FILE *f = fopen(argv[3], "wb");
+            if (!f)
+                return 5;
+            for (size_t r = 0; r + 6 <= rays.size(); r += 6) {
+                it->init(Ray(Vector3D(rays[r], rays[r + 1], rays[r + 2]), Vector3D(rays[r + 3], rays[r + 4], rays[r + 5])));
+                std::vector<float> rec;
+                int32_t count = 0;
+                for (; !it->isAtEnd(); it->next(), count++) {
+                    const Span &sp = **it;
+                    int32_t m0 = mi(sp.startMaterial), m1 = mi(sp.endMaterial);
+                    float a[4] = {sp.start, sp.startNormal.x, sp.startNormal.y, sp.startNormal.z};
+                    float b[4] = {sp.end, sp.endNormal.x, sp.endNormal.y, sp.endNormal.z};
+                    float m0f, m1f;
+                    memcpy(&m0f, &m0, 4), memcpy(&m1f, &m1, 4);
+                    rec.insert(rec.end(), a, a + 4), rec.push_back(m0f);
+                    rec.insert(rec.end(), b, b + 4), rec.push_back(m1f);
+                }
+                fwrite(&count, 4, 1, f);
+                fwrite(rec.data(), 4, rec.size(), f);
+            }
+            fclose(f);
+            return 0;
+        }
+        if (!strcmp(argv[1], "tex") && argc == 5) {
+            std::unique_ptr<Texture> mb(new MirrorBallSkymapTexture(new ImageTexture(Image(argv[2]))));
+            Checker user;
+            std::vector<float> pts = read_f32(argv[3]);
+            FILE *f = fopen(argv[4], "wb");
+            if (!f)
+                return 5;
+            const size_t n = pts.size() / 3;
+            std::vector<Vector3D> P;
+            for (size_t k = 0; k < n; k++) P.push_back(Vector3D(pts[3 * k], pts[3 * k + 1], pts[3 * k + 2]));
+            std::vector<Color> C(n);
+            std::vector<float> V(n);
+            mb->getColors(P.data(), n, C.data(), V.data()); /* one device call for all points */
+            for (size_t k = 0; k < n; k++) {
+                if (k < 4) { /* the per-point virtuals give the same bits */
+                    Color c = mb->getColor(P[k]);
+                    float v = mb->getFloat(P[k]);
+                    if (memcmp(&c, &C[k], sizeof c) || memcmp(&v, &V[k], 4))
+                        return 6;
+                }
+                Color u = user.getColor(P[k]);
+                float rec[8] = {C[k].x, C[k].y, C[k].z, V[k], u.x, u.y, u.z, user.getFloat(P[k])};
+                fwrite(rec, 4, 8, f);
+            }
+            fclose(f);
             return 0;
         }
         Renderer renderer(world.get());

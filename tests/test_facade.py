@@ -47,3 +47,61 @@ def test_facade_render_bitexact(facade_bin, tmp_path):
     got = np.fromfile(out, dtype=np.float32).reshape(-1, 3)
     want = pt.render(scenes.scene_p1(), W, H, spp, depth).reshape(-1, 3)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_facade_span_iterator_matches_oracle(facade_bin, tmp_path):
+    """world->makeSpanIterator() through the facade (pt_query_spans): init(Ray)
+    / isAtEnd / operator* / next give the reference's span lists, bit for bit
+    against the oracle (which tests/test_oracle_golden.py pins to the reference)."""
+    import oracle_py as O
+    import zoo as T
+    from pathtrace.scene import to_text
+    rays = T.random_rays(64, seed=5)
+    rp, out = str(tmp_path / "rays.bin"), str(tmp_path / "spans.bin")
+    rays.tofile(rp)
+    r = subprocess.run([facade_bin, "spans", rp, out], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    want = O.spans(to_text(scenes.scene_p1(), str(tmp_path)), rays)
+    buf = open(out, "rb").read()
+    pos, matmap = 0, {}
+    for spans in want:
+        c = int(np.frombuffer(buf, dtype=np.int32, count=1, offset=pos)[0])
+        pos += 4
+        assert c == len(spans)
+        for (a, m0, b, m1) in spans:
+            rec = np.frombuffer(buf, dtype=np.float32, count=10, offset=pos)
+            pos += 40
+            np.testing.assert_array_equal(rec[[0, 1, 2, 3, 5, 6, 7, 8]].view(np.uint32),
+                                          np.concatenate([a, b]).view(np.uint32))
+            for mine, theirs in ((rec[4:5].view(np.int32)[0], m0), (rec[9:10].view(np.int32)[0], m1)):
+                assert matmap.setdefault(int(mine), theirs) == theirs  # one Material per material id
+    assert pos == len(buf)
+
+
+@pytest.mark.gpu
+def test_facade_texture_virtuals(facade_bin, tmp_path):
+    """Texture::getColor / getFloat through the facade (pt_tex_eval) for a
+    mirror-ball sky map of the reference's test2.hdr, against the oracle; and a
+    reference-style user subclass that overrides getColor only (host-side,
+    getFloat = the reference's default mean)."""
+    import oracle_py as O
+    import zoo as T
+    from pathtrace.scene import (ColorTexture, Image, ImageTexture, Material, MirrorBallSkymapTexture, Sphere,
+                                 to_text)
+    hdr = os.path.join(ROOT, "assets", "test2.hdr")
+    pts = T.texture_points(256, seed=4)
+    pp, out = str(tmp_path / "pts.bin"), str(tmp_path / "tex.bin")
+    pts.tofile(pp)
+    r = subprocess.run([facade_bin, "tex", hdr, pp, out], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, dtype=np.float32).reshape(-1, 8)
+    scene = Sphere((0, 0, -4), 1, Material(ColorTexture(0), ColorTexture(0),
+                                          MirrorBallSkymapTexture(ImageTexture(Image(path=hdr)))))
+    txt = to_text(scene, str(tmp_path))
+    kinds = [ln.split()[2] for ln in txt.splitlines() if ln.startswith("tex ")]
+    want = O.tex_eval(txt, pts)[kinds.index("mirrorball")]
+    np.testing.assert_array_equal(got[:, :4].view(np.uint32), want.view(np.uint32))
+    chk = np.where((np.floor(pts).astype(np.int64).sum(axis=1) % 2) != 0, 1.0, 0.25).astype(np.float32)
+    np.testing.assert_array_equal(got[:, 4], chk)
+    np.testing.assert_array_equal(got[:, 7], ((chk + chk) + chk) * np.float32(1.0 / 3.0))

@@ -290,6 +290,22 @@ def test_sample_split_sums(built, tmp_path):
     assert np.all(e <= 1e-6), e
 
 
+def test_sample_split_block_path(built, tmp_path):
+    """The sample split's real shape: shares of more than 64 samples, a
+    multiple of 32, the second at a nonzero sample_begin -- the block-staged
+    path (one launch, 32-sample block partials in the kernel, reduce mode 2),
+    not the per-sample staging of small shares.  Each share's sums equal the
+    oracle's per-sample values summed in the fast order's blocks bit for bit."""
+    root = scenes.scene_p1()
+    W, H, S, depth = 16, 8, 256, 8
+    per = O.render(to_text(root, str(tmp_path)), W, H, S, depth, order=O.ORDER_FAST, per_sample=True)
+    ds = pt.DeviceScene(root)
+    for b, c in [(0, 128), (128, 128)]:
+        g, st = pt.render(ds, W, H, c, depth, sample_begin=b, sum_only=True, stats=True)
+        assert st["launches"] == 1
+        assert_bits(g.reshape(-1, 3), block_sum(per[:, b:b + c]), "samples %d..%d" % (b, b + c - 1))
+
+
 @pytest.mark.parametrize("name", ["C3", "C2", "C5"])
 def test_config_scale_vs_reference(built, name, tmp_path):
     """Each benchmark config at its real spp and depth against the UNMODIFIED

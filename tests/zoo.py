@@ -143,3 +143,23 @@ def union_zoo():
     for n in [(0, 0, -1), (0, 0, 1), (0, -1, 0), (0, 1, 0), (1, 0, 0), (-1, 0, 0)]:
         objs.append(Plane(n, 60, sky))
     return union_array(objs)
+
+
+def texture_points(n=2048, seed=13):
+    """Lookup points for the texture query goldens (pt_tex_eval): random points
+    in a box, unit directions (the sky maps' domain), points on the cube-face
+    diagonals and axes (skybox face ties), exact zeros and far points."""
+    rng = np.random.default_rng(seed)
+    box = rng.uniform(-3, 3, size=(n // 2, 3))
+    d = rng.normal(size=(n // 4, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    ties = rng.choice([-1.0, 1.0], size=(n // 8, 3)) * rng.uniform(0.1, 2, size=(n // 8, 1))
+    ties[: n // 16, rng.integers(0, 3)] = 0.0
+    axes = np.concatenate([np.eye(3), -np.eye(3), np.zeros((1, 3))]) * np.array([[1.0], [2.5], [0.3], [1.0], [7.0],
+                                                                                [0.5], [1.0]])
+    far = rng.normal(size=(n - len(box) - len(d) - len(ties) - len(axes), 3)) * 1e4
+    return np.concatenate([box, d, ties, axes, far]).astype(np.float32)
+
+
+# scenes of the texture query goldens (tests/golden/tex_eval.npz)
+TEX_EVAL_SCENES = ["texture_zoo", "texture_transc_zoo"]
