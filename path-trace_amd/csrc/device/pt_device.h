@@ -1546,6 +1546,7 @@ struct Counters
     u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow, dark, mid;
 #ifdef PT_PHASE_TIMING
     u64 ph[7]; /* cycles: generation, its attempts, fast pass, slow pass, accumulation, burst total, sample total */
+    u64 sp[2]; /* cycles of the spine: its span queries, the rest of its node work outside bursts */
     u64 np[8]; /* events: bursts, loop iterations, (unused), fast passes, slow passes, accumulations, fast lanes, slow lanes */
 #define PT_CNT(c, k, v) (c).np[k] += (v)
 #else
@@ -1950,7 +1951,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 }
             }
             PT_ACC(cnt, 1, tg); /* the attempts alone (slot 1) */
+#ifdef PT_FULL_STATS /* diagnostic builds: per-round attempt statistics */
             cadd(cnt.rounds, 1u);
+#endif
             if (DEFERRED && KR0)
                 PT_MARK(14); /* the diffuse (scatter coefficient 1) variant */
             int m; /* attempts consumed this round, 1..64*PT_KATT */
@@ -2039,9 +2042,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     child.depth = depth - 1;
                 }
             }
+#ifdef PT_FULL_STATS
             cadd(cnt.attempts, (u32)m);
-            cadd(cnt.leaf, (u32)np);
-            cadd(cnt.dark, (u32)(np - nk));
+#endif
             f_n += nk;
             npos += np;
             nkeep += nk;
@@ -2293,6 +2296,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     /* the run's end: retval + the pairwise tree of the 64 lane sums */
     if (!STRICT && npos > 0)
         retval = wave_tree_sum3_add(lsum, retval);
+    /* leaf children of the burst (each one span query) and the dark ones among them */
+    cadd(cnt.leaf, (u32)npos);
+    cadd(cnt.dark, (u32)(npos - nkeep));
     f.retval = retval;
     f.i = i + npos;
     return reason;
@@ -2438,9 +2444,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
             if (sp == 0) {
                 found = cam.hit != 0, t = cam.t, ref = cam.ref, ex = cam.ex != 0;
             } else {
-#ifdef PT_SPINE_TIMING
                 PT_T0(tq);
-#endif
                 typename S::Root::Ctx ctx;
                 S::Root::prep(ctx, o, e);
 #ifdef PT_FAST_SPINE /* per scene, pt_scene_set_fast_spine */
@@ -2448,8 +2452,9 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
 #else
                 found = first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
 #endif
-#ifdef PT_SPINE_TIMING
-                PT_ACC(cnt, 0, tq);
+#ifdef PT_PHASE_TIMING
+                cnt.sp[0] += __builtin_amdgcn_s_memtime() - tq;
+                cnt.sp[1]++;
 #endif
             }
             if (!found) {
@@ -2473,13 +2478,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 n = nn;
                 ior = (float)(1.0 / (double)S::ior(mat, e));
             }
-#ifdef PT_SPINE_TIMING
-            PT_T0(tm);
-#endif
             const V3 retval = S::emis(mat, hit, e);
-#ifdef PT_SPINE_TIMING
-            PT_ACC(cnt, 1, tm);
-#endif
             f.hit = hit, f.n = n, f.mat = mat, f.retval = retval, f.add = 1.0f;
             const float strength = unif(f.strength);
             if (uni(f.depth) <= 0 || strength < EPS) {
@@ -2488,13 +2487,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 continue;
             }
             cnt.shaded++;
-#ifdef PT_SPINE_TIMING
-            PT_T0(tr0);
-#endif
             const float rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
-#ifdef PT_SPINE_TIMING
-            PT_ACC(cnt, 2, tr0);
-#endif
             f.rf = rf;
             if (rf > EPS) {
                 V3 rd = refract(d, ior, n);
@@ -2638,6 +2631,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         cnt.ph[k] = 0;
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
+    cnt.sp[0] = cnt.sp[1] = 0;
 #endif
     const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
@@ -2746,6 +2740,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             atomicAdd(&stats[8 + k], cnt.ph[k]);
         for (int k = 0; k < 8; k++)
             atomicAdd(&stats[16 + k], cnt.np[k]);
+        atomicAdd(&stats[30], cnt.sp[0]);
+        atomicAdd(&stats[31], cnt.sp[1]);
 #endif
     }
 }

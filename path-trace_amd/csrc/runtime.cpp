@@ -711,6 +711,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             for (int k = 16; k < 24; k++)
                 fprintf(stderr, " %llu", (unsigned long long)c[k]);
             fprintf(stderr, " %llu", (unsigned long long)c[25]); /* whole chunk loop */
+            fprintf(stderr, " %llu %llu", (unsigned long long)c[30], (unsigned long long)c[31]); /* spine queries */
             fprintf(stderr, "\n");
         }
         st->sphere_tests = st->queries * (uint64_t)g.n_spheres;

@@ -30,6 +30,8 @@ for line in r.stderr.splitlines():
         if len(v) >= 16 and v[15]:
             print("%-12s %6.1f%%  (of the whole chunk loop: lane-parallel camera queries, lane samples, writes)" %
                   ("sample/loop", 100.0 * tot / v[15]))
+        if len(v) >= 18 and v[17]:
+            print("%-12s %6.1f%%  (%.0f cycles per query)" % ("spine-query", 100.0 * v[16] / tot, v[16] / v[17]))
         if len(v) >= 15:
             import json as _j
             smp = _j.loads(r.stdout.strip().splitlines()[-1])["samples"]
