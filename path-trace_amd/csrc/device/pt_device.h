@@ -1804,7 +1804,7 @@ __device__ __forceinline__ int replay(u64 A, u64 F, u64 NL, int rem, int &fails,
  * the next child's ray into `child` when that child must recurse (it draws
  * random numbers, so it runs on the spine). */
 template <class S, bool STRICT, bool DEFERRED, bool KR0>
-__device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
+__device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, const u64 *jl,
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
     float4 *const ring = L.ring;
@@ -1821,7 +1821,10 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const float aN = unif(add / (float)N);                /* addFactor / scatter_ray_count                       */
     const float abs_rc = unif(length(rc));
     const bool child_leaf_depth = depth - 1 <= 0;
-    const u64 ginc = G3l * LCG_INC;
+    /* lane l's state 3l draws into the round (attempt l): its jump (A, G)
+     * is read from LDS where a round needs it, not held in registers */
+    const u64 jA = jl[0], jG = jl[1] * LCG_INC;
+    auto lane_state = [&]() { return jA * rng.st + jG; };
     const u64 A64 = jump[128], g64inc = jump[129] * LCG_INC;   /* 64 attempts = 192 draws  */
     const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * LCG_INC; /* a full round */
     int fails = 0, reason = -1;
@@ -1918,7 +1921,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             };
             if (DEFERRED) {
                 /* pairs of attempts in packed f32 */
-                u64 sk = A3l * rng.st + ginc;
+                u64 sk = lane_state();
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k += 2) {
                     if (k)
@@ -1938,7 +1941,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     sk = sk1;
                 }
             } else {
-                u64 sk = A3l * rng.st + ginc;
+                u64 sk = lane_state();
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k++) {
                     if (k)
@@ -1977,7 +1980,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 Attempt at[PT_KATT];
                 u64 Dm[PT_KATT];
                 {
-                    u64 sk = A3l * rng.st + ginc;
+                    u64 sk = lane_state();
 #pragma unroll
                     for (int k = 0; k < PT_KATT; k++) {
                         if (k)
@@ -2310,7 +2313,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
  * normalised direction / factor are computed per child at trace time (same
  * arithmetic, same bits) with every lane busy. */
 template <class S, bool STRICT>
-__device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, u64 A3l, u64 G3l,
+__device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, const u64 *jl,
                                      const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
     const float sNa = unif((unif(f.strength) / (float)uni(f.N)) * unif(f.add));
@@ -2320,11 +2323,11 @@ __device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restri
     int r;
     if (deferred) {
         if (unif(f.sc) == 1.0f)
-            r = burst_t<S, STRICT, true, true>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+            r = burst_t<S, STRICT, true, true>(e, rng, jump, jl, L, f, child, cnt);
         else
-            r = burst_t<S, STRICT, true, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+            r = burst_t<S, STRICT, true, false>(e, rng, jump, jl, L, f, child, cnt);
     } else {
-        r = burst_t<S, STRICT, false, false>(e, rng, jump, A3l, G3l, L, f, child, cnt);
+        r = burst_t<S, STRICT, false, false>(e, rng, jump, jl, L, f, child, cnt);
     }
     PT_ACC(cnt, 5, t0);
     return r;
@@ -2420,7 +2423,7 @@ __device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 d, const
 
 template <class S, int MAXD, bool STRICT>
 __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, const WaveLds &L,
-                                           const u64 *__restrict__ jump, u64 A3l, u64 G3l, Counters &cnt,
+                                           const u64 *__restrict__ jump, const u64 *jl, Counters &cnt,
                                            const CamHit &cam)
 {
     Rng rng;
@@ -2530,7 +2533,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 continue;
             }
             if (unif(f.sc) > EPS) {
-                int why = burst<S, STRICT>(e, rng, jump, A3l, G3l, L, f, F[sp + 1], cnt);
+                int why = burst<S, STRICT>(e, rng, jump, jl, L, f, F[sp + 1], cnt);
                 if (why != B_NONLEAF) {
                     result = univ(f.retval);
                     phase = PH_RETURN;
@@ -2619,10 +2622,20 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     __shared__ unsigned char sbuf[PT_WPW][PT_SCAP];
     __shared__ unsigned char mbuf[PT_WPW][PT_SCAP];
     __shared__ Counters cbuf[PT_WPW];
+    /* a chunk's lanes while the wave walks its samples one by one: (pixel,
+     * sample | hit << 30 | exit << 31, camera t, camera ref) and the results,
+     * in LDS rather than in registers that would stay live through every
+     * burst (the allocator spilled them to scratch) */
+    __shared__ uint4 lbuf[PT_WPW][64];
+    __shared__ float obuf[PT_WPW][64 * 3];
+    /* lane l's engine jump of 3l draws (A, G): read by each generation round */
+    __shared__ u64 jbuf[64][2];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const u64 t_start = __builtin_amdgcn_s_memrealtime(); /* 100 MHz: wave lifetimes, stats[26..29] */
     const Env e = {P, imgs};
-    const u64 A3l = jump[2 * lane], G3l = jump[2 * lane + 1];
+    if (wave == 0)
+        jbuf[lane][0] = jump[2 * lane], jbuf[lane][1] = jump[2 * lane + 1];
+    __syncthreads();
     Counters &cnt = cbuf[wave];
     cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = cnt.slow = cnt.dark = 0;
     cnt.mid = 0;
@@ -2674,22 +2687,27 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             cnt.queries += (u64)(__popcll(D) + __popcll(Q2));
             cnt.shaded += (u64)__popcll(SH);
         }
-        V3 mine = lres; /* valid where ldone */
+        /* park the lanes' state in LDS for the walks below */
+        uint4 *const lb = lbuf[wave];
+        float *const ob = obuf[wave];
+        lb[lane] = make_uint4((u32)lpix, (u32)ls | ((u32)ch.hit << 30) | ((u32)ch.ex << 31), __float_as_uint(ch.t),
+                              ch.ref);
+        ob[3 * lane] = lres.x, ob[3 * lane + 1] = lres.y, ob[3 * lane + 2] = lres.z; /* valid where ldone */
         /* the other items, one after another by the whole wave; only this mask
-         * and the lanes' (pixel, sample) stay live across the walks, not the
-         * launch fields item_slot needs */
+         * stays live across the walks */
         for (u64 todo = __ballot(lvalid) & ~__ballot(ldone); todo; todo &= todo - 1) {
             const int j = uni(__builtin_ctzll(todo));
             PT_T0(tt);
-            const CamHit cam = {__builtin_amdgcn_readlane(ch.hit, j), rdlane(ch.t, j),
-                                (u32)__builtin_amdgcn_readlane((int)ch.ref, j), __builtin_amdgcn_readlane(ch.ex, j)};
-            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, __builtin_amdgcn_readlane(lpix, j),
-                                                 __builtin_amdgcn_readlane(ls, j), stk[wave], L, jump, A3l, G3l, cnt,
-                                                 cam);
+            const uint4 q = lb[j];
+            const int qy = uni((int)q.y);
+            const CamHit cam = {(qy >> 30) & 1, unif(__uint_as_float(q.z)), (u32)uni((int)q.w), (int)((u32)qy >> 31)};
+            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni((int)q.x), qy & 0x3FFFFFFF, stk[wave], L, jump,
+                                                 jbuf[lane], cnt, cam);
             PT_ACC(cnt, 6, tt);
             if (lane == j)
-                mine = c;
+                ob[3 * j] = c.x, ob[3 * j + 1] = c.y, ob[3 * j + 2] = c.z;
         }
+        const V3 mine = mk(ob[3 * lane], ob[3 * lane + 1], ob[3 * lane + 2]);
         const long long my = item0 + lane;
         if (lp.block_sums) {
             /* the chunk is one 32-sample block of one slot (slot-major, chunk
@@ -2755,7 +2773,8 @@ template <class S, int MAXD>
 __device__ constexpr int min_workgroups()
 {
     constexpr int lds = PT_WPW * ((MAXD + 1) * (int)sizeof(Frame) + 16 * PT_RCAP + 2 * PT_SCAP +
-                                  (int)sizeof(Counters) + (int)sizeof(typename S::Root::Ctx));
+                                  (int)sizeof(Counters) + (int)sizeof(typename S::Root::Ctx) + 64 * (16 + 12)) +
+                        64 * 16;
     constexpr int alloc = (lds + 1279) / 1280 * 1280; /* gfx950 LDS allocation unit (measured) */
     constexpr int n = 160 * 1024 / alloc;
     return n < 1 ? 1 : n > 5 ? 5 : n;
