@@ -216,6 +216,13 @@ int pt_scene_set_occupancy(pt_scene *s, int workgroups_per_cu);
  * where they often do (C3 spine: -0.9 %).  Takes effect at the next
  * compile/render. */
 int pt_scene_set_fast_spine(pt_scene *s, int on);
+/* MI355X tuning knob, no reference counterpart: each lane of a chunk walks its
+ * own sample's ray tree when no node of it has a scatter loop (mirrors, glass,
+ * emitters), with `frames` (1..8) register frames for pending nodes; samples
+ * that need a scatter loop or a deeper stack go to the wave as before (same
+ * bits either way).  Pays where such trees are common (C5's glass ball), costs
+ * registers elsewhere.  0 = off.  Takes effect at the next compile/render. */
+int pt_scene_set_lane_walk(pt_scene *s, int frames);
 /* Key of the code object for this scene/depth (hex string, static storage). */
 const char *pt_scene_kernel_key(pt_scene *s, int depth);
 

@@ -2421,6 +2421,168 @@ __device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 d, const
     return true;
 }
 
+#ifdef PT_LANE_WALK
+/* A whole sample walked by its own lane when its ray tree has no scatter loop
+ * (every node's scatter_coefficient <= eps: mirrors, glass, emitters --
+ * C5's glass ball and sky box).  Such nodes draw no random numbers, so the
+ * lanes of a chunk walk their trees independently: depth first, the
+ * refraction child before the mirror child, each node the spine's own
+ * statements (trace_sample PH_ENTER / PH_SETUP / PH_LOOP / PH_RETURN) and the
+ * same fold retval = (e + w_R r_R) + w_M r_M.  Pending nodes live in a
+ * PT_LANE_WALK-deep stack of register frames, shifted on push and pop (a
+ * per-lane index would put it in scratch).  A lane whose tree needs a scatter
+ * loop or a deeper stack gives the sample back to the wave (returns false).
+ * nq / nsh = queries / shaded nodes, for the statistics. */
+struct WalkFrame
+{
+    int mode;          /* 0: in R, M pending; 1: in R, no M; 2: in M */
+    V3 part, wR, wM;   /* e (+ w_R r_R once R is done), the children's weights */
+    V3 mo, md;         /* the M child's ray */
+    float ms;          /* its strength */
+    int mdep;          /* its depth */
+};
+template <class S>
+__device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 d0, const CamHit &ch, V3 &res, int &nq,
+                                          int &nsh)
+{
+    constexpr int K = PT_LANE_WALK;
+    WalkFrame F[K];
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        F[k].mode = 0;
+    int sp = 0;
+    V3 o = mk(0, 0, 0), d = d0, r = mk(0, 0, 0);
+    int dep = depth0;
+    float str = 1.0f;
+    bool first = true, descend = true, ok = true, done = false;
+    nq = 0, nsh = 0;
+    auto push = [&](const WalkFrame &w) {
+#pragma unroll
+        for (int k = K - 1; k > 0; k--)
+            F[k] = F[k - 1];
+        F[0] = w;
+        sp++;
+    };
+    auto pop = [&]() {
+#pragma unroll
+        for (int k = 0; k < K - 1; k++)
+            F[k] = F[k + 1];
+        sp--;
+    };
+    while (ok && !done) {
+        if (descend) {
+            /* PH_ENTER */
+            nq++;
+            float t = 0.0f;
+            u32 ref = 0;
+            bool ex = false, found;
+            if (first) {
+                found = ch.hit != 0, t = ch.t, ref = ch.ref, ex = ch.ex != 0;
+                first = false;
+            } else {
+                typename S::Root::Ctx ctx;
+                S::Root::prep_l(ctx, o, e);
+                found = lane_first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+            }
+            if (!found) {
+                r = mk(0, 0, 0);
+                descend = false;
+                continue;
+            }
+            const V3 hit = o + t * d;
+            const int mat = ref_mat(ref);
+            V3 nn = S::Root::normal(ref_prim(ref), t, o, d, e);
+            if (ref & FLIP)
+                nn = -nn;
+            float ior;
+            V3 n;
+            if (ex) {
+                n = -nn;
+                ior = S::ior(mat, e);
+            } else {
+                n = nn;
+                ior = (float)(1.0 / (double)S::ior(mat, e));
+            }
+            const V3 retval = S::emis(mat, hit, e);
+            if (dep <= 0 || str < EPS) {
+                r = retval;
+                descend = false;
+                continue;
+            }
+            nsh++;
+            const float rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
+            bool hasR = false;
+            V3 rd = mk(0, 0, 0), wR = mk(0, 0, 0);
+            float sR = 0.0f, add = 1.0f;
+            if (rf > EPS) {
+                rd = refract(d, ior, n);
+                if (!is_zero(rd)) {
+                    const V3 tr = S::trans(mat, hit, e);
+                    wR = (1.0f * rf) * tr; /* addFactor * refractFactor * transmit */
+                    sR = str * rf * 1.0f * length(tr);
+                    hasR = true;
+                    add = 1.0f * (1.0f - rf); /* PH_RETURN's addFactor *= 1 - rf */
+                }
+            }
+            /* PH_SETUP */
+            bool hasM = !(add < EPS);
+            WalkFrame w;
+            w.part = retval, w.wR = wR;
+            w.wM = mk(0, 0, 0), w.mo = hit, w.md = mk(0, 0, 0), w.ms = 0.0f, w.mdep = dep - 1;
+            if (hasM) {
+                const float sc = clamp01(S::scat(mat, hit, e));
+                if (sc > EPS) { /* a scatter loop: the wave's burst machinery */
+                    ok = false;
+                    continue;
+                }
+                /* N = 1 (sc <= eps) */
+                const V3 rc = S::refl(mat, hit, e);
+                const V3 refl = reflect(d, n);
+                const float factor = 1.0f - (1.0f - dot(refl, n)) * sc;
+                w.wM = ((add / 1.0f) * factor) * rc;
+                w.md = refl;
+                w.ms = (((str / 1.0f) * add) * factor) * length(rc);
+            }
+            if (!hasR && !hasM) {
+                r = retval;
+                descend = false;
+                continue;
+            }
+            if (sp == K) { /* deeper than the register stack */
+                ok = false;
+                continue;
+            }
+            w.mode = hasR ? (hasM ? 0 : 1) : 2;
+            push(w);
+            if (hasR)
+                o = hit, d = rd, str = sR, dep = dep - 1;
+            else
+                o = w.mo, d = w.md, str = w.ms, dep = w.mdep;
+        } else {
+            /* PH_RETURN: fold the finished child into the top frame */
+            if (sp == 0) {
+                done = true;
+                continue;
+            }
+            if (F[0].mode == 0) {
+                F[0].part = F[0].part + F[0].wR * r;
+                F[0].mode = 2;
+                o = F[0].mo, d = F[0].md, str = F[0].ms, dep = F[0].mdep;
+                descend = true;
+            } else {
+                r = F[0].part + (F[0].mode == 1 ? F[0].wR : F[0].wM) * r;
+                pop();
+            }
+        }
+    }
+    if (!ok)
+        return false;
+    const V3 z = mk(0, 0, 0);
+    res = (z + r) / 1.0f;
+    return true;
+}
+#endif
+
 template <class S, int MAXD, bool STRICT>
 __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, const WaveLds &L,
                                            const u64 *__restrict__ jump, const u64 *jl, Counters &cnt,
@@ -2679,13 +2841,29 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             bool ex = false;
             ch.hit = lane_first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
             ch.ex = ex ? 1 : 0;
+#ifdef PT_LANE_WALK /* per scene, pt_scene_set_lane_walk */
+            ldone = lane_walk<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
+#else
             ldone = lane_sample<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
+#endif
         }
         {
             /* statistics of the samples finished by their lane */
+#ifdef PT_LANE_WALK
+            {
+                /* per-lane counts: a wave sum of small integers */
+                int q = ldone ? lq : 0, h = ldone ? lsh : 0;
+#pragma unroll
+                for (int w = 32; w >= 1; w >>= 1)
+                    q += __shfl_xor(q, w), h += __shfl_xor(h, w);
+                cnt.queries += (u64)(u32)uni(q);
+                cnt.shaded += (u64)(u32)uni(h);
+            }
+#else
             const u64 D = __ballot(ldone), Q2 = __ballot(ldone && lq == 2), SH = __ballot(ldone && lsh);
             cnt.queries += (u64)(__popcll(D) + __popcll(Q2));
             cnt.shaded += (u64)__popcll(SH);
+#endif
         }
         /* park the lanes' state in LDS for the walks below */
         uint4 *const lb = lbuf[wave];

@@ -69,6 +69,7 @@ struct SceneImpl
     int default_tex[2] = {-1, -1}; /* lazily created ColorTexture(0), ColorTexture(1) */
     int wg_per_cu = 0;             /* resident workgroups per CU the kernel is built for (0 = auto) */
     int fast_spine = 0;            /* spine queries try all spans + the fast checks first */
+    int lane_walk = 0;             /* register frames of the per-lane scatter-free tree walk (0 = off) */
     std::map<int, std::unique_ptr<DeviceState>> devices;
     std::string last_key;
     void clear()

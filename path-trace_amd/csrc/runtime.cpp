@@ -1094,6 +1094,16 @@ int pt_scene_set_fast_spine(pt_scene *s, int on)
     });
 }
 
+int pt_scene_set_lane_walk(pt_scene *s, int frames)
+{
+    return guard([&] {
+        if (frames < 0 || frames > 8)
+            throw Error(PT_ERR_ARG, "lane walk frames must be in [0, 8]");
+        S(s).lane_walk = frames;
+        return PT_OK;
+    });
+}
+
 const char *pt_scene_kernel_key(pt_scene *s, int depth)
 {
     thread_local std::string k;

@@ -36,7 +36,7 @@ class DeviceScene:
     """A pt_scene built from a Python scene graph through the C-ABI
     constructors (one pt_* call per reference constructor)."""
 
-    def __init__(self, root: Object, workgroups_per_cu: int = 0, fast_spine: bool = False):
+    def __init__(self, root: Object, workgroups_per_cu: int = 0, fast_spine: bool = False, lane_walk: int = 0):
         L = _lib.lib()
         self._h = L.pt_scene_create()
         if not self._h:
@@ -45,6 +45,8 @@ class DeviceScene:
             _lib.check(L.pt_scene_set_occupancy(self._h, int(workgroups_per_cu)))
         if fast_spine:
             _lib.check(L.pt_scene_set_fast_spine(self._h, 1))
+        if lane_walk:
+            _lib.check(L.pt_scene_set_lane_walk(self._h, int(lane_walk)))
         self._img = {}
         self._mat = {}
         self.root = root

@@ -186,12 +186,14 @@ class Config:
     note: str = ""
     wg_per_cu: int = 0  # pt_scene_set_occupancy (0 = as many as LDS allows)
     fast_spine: bool = False  # pt_scene_set_fast_spine
+    lane_walk: int = 0  # pt_scene_set_lane_walk (register frames; 0 = off)
 
     def device_scene(self, procedural: bool = False):
         """The config's scene as a DeviceScene, built at the config's occupancy."""
         from . import DeviceScene
         root = self.scene(procedural=True) if procedural else self.scene()
-        return DeviceScene(root, workgroups_per_cu=self.wg_per_cu, fast_spine=self.fast_spine)
+        return DeviceScene(root, workgroups_per_cu=self.wg_per_cu, fast_spine=self.fast_spine,
+                           lane_walk=self.lane_walk)
 
     @property
     def screen(self):
@@ -204,8 +206,11 @@ CONFIGS: Dict[str, Config] = {
     "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG"),
     "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene over 8 GPUs + RCCL framebuffer reduce"),
     # C5 at 2 workgroups per CU: its 14-primitive tree spills 1032 VGPRs at the
-    # default cap of 128 and its time is spine walks through the glass ball:
-    # 119 -> 277 Msamples/s on one MI355X
+    # default cap of 128 (119 -> 277 Msamples/s on one MI355X, round 2).  Its
+    # glass-ball trees have no scatter loop: lanes walk them with 2 register
+    # frames instead of the wave (bench-like subset at 256 spp 685 -> 2330
+    # Msamples/s, glass disk 65 -> 708; 3 frames 2311, 4 frames 2164)
     "C5": Config("C5", 3840, 2160, 8192, 16, scene_c5, gpus=8,
-                 note="demo world + test.hdr spherical env + sky01 skybox", wg_per_cu=2, fast_spine=True),
+                 note="demo world + test.hdr spherical env + sky01 skybox", wg_per_cu=2, fast_spine=True,
+                 lane_walk=2),
 }

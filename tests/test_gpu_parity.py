@@ -110,6 +110,39 @@ def test_union_rule_overlaps_and_ties_bitexact(built, tmp_path, order):
     assert_bits(g, o, "union zoo, %s order vs oracle" % order)
 
 
+LANE_WALK_CASES = [("csg_zoo", 6, 1), ("csg_zoo", 6, 2), ("scene_p0", 4, 2), ("texture_zoo", 5, 2),
+                   ("union_zoo", 6, 3)]
+
+
+@pytest.mark.parametrize("builder,depth,frames", LANE_WALK_CASES)
+def test_lane_walk_bitexact(built, tmp_path, builder, depth, frames):
+    """pt_scene_set_lane_walk: lanes walk their own scatter-free ray trees
+    (mirror / glass / emitter nodes) with a few register frames and hand
+    scatter loops and deeper trees to the wave -- the same bits as the oracle
+    (1 frame: most glass trees go back to the wave; 2-3: most finish in lanes)."""
+    root = T.build(builder)
+    W, H, spp = 40, 24, 3
+    g = pt.render(pt.DeviceScene(root, lane_walk=frames), W, H, spp, depth, order="fast")
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_FAST)
+    assert_bits(g, o, "lane walk %d, %s vs oracle" % (frames, builder))
+
+
+def test_lane_walk_c5_same_bits(built):
+    """C5 (glass ball, sky box with the spherical sky map, skybox sphere) at its
+    depth: the per-lane walk gives the wave walk's bits, transcendental
+    textures included."""
+    cfg = scenes.CONFIGS["C5"]
+    rng = np.random.default_rng(3)
+    pix = np.sort(rng.choice(cfg.width * cfg.height, 2048, replace=False)).astype(np.int32)
+    disk = (1080 + np.arange(-20, 20)[:, None]) * cfg.width + (2460 + np.arange(-20, 20)[None, :])
+    pix = np.unique(np.concatenate([pix, disk.ravel().astype(np.int32)]))
+    imgs = []
+    for frames in (0, cfg.lane_walk or 2):
+        ds = pt.DeviceScene(cfg.scene(), workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine, lane_walk=frames)
+        imgs.append(pt.render(ds, cfg.width, cfg.height, 16, cfg.depth, screen=cfg.screen, pixels=pix))
+    assert_bits(imgs[1], imgs[0], "C5 lane walk vs wave walk")
+
+
 @pytest.mark.parametrize("builder,depth", [("csg_zoo", 6), ("scene_p1", 8), ("union_zoo", 6)])
 def test_fast_spine_bitexact(built, tmp_path, builder, depth):
     """pt_scene_set_fast_spine: wave-walked queries take every span and the
@@ -127,7 +160,7 @@ def test_full_1080p_frame_on_sampled_pixels(built, tmp_path):
     every pixel; the oracle checks 1500 hashed pixels bit for bit."""
     cfg = scenes.CONFIGS["C3"]
     root = cfg.scene()
-    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen, stats=True)
+    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine, lane_walk=cfg.lane_walk), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen, stats=True)
     rng = np.random.default_rng(7)
     pix = np.sort(rng.choice(cfg.width * cfg.height, 1500, replace=False)).astype(np.int32)
     o = O.render(to_text(root, str(tmp_path)), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen,
@@ -145,7 +178,7 @@ def test_benchmark_configs_on_sampled_pixels(built, tmp_path, name, spp, npix):
     the full frame on the GPU, hashed pixels bit for bit against the oracle."""
     cfg = scenes.CONFIGS[name]
     root = cfg.scene()
-    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
+    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine, lane_walk=cfg.lane_walk), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
     assert st["samples"] == cfg.width * cfg.height * spp
     rng = np.random.default_rng(11)
     pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
@@ -246,7 +279,7 @@ def test_c4_eight_shards_on_one_gpu(built, tmp_path):
     (replaces the reference's block farm, src/test.cpp:520-778)."""
     cfg = scenes.CONFIGS["C4"]
     root = cfg.scene()
-    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine)
+    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine, lane_walk=cfg.lane_walk)
     W, H, spp = cfg.width, cfg.height, 2
     full = pt.render(ds, W, H, spp, cfg.depth, screen=cfg.screen).reshape(-1, 3)
     acc = np.zeros_like(full)
