@@ -74,7 +74,8 @@ struct PtLaunch
     int sample_major;   /* item order: 1 = consecutive items are consecutive slots
                            at one sample, 0 = a slot's samples are consecutive    */
     int block_sums;     /* stage one partial per 32-sample block (slot-major,
-                           chunk 32, nsamp % 32 == 0), else one value per sample */
+                           chunk 32 or 64, nsamp % chunk == 0), else one value
+                           per sample */
 };
 
 struct Env
@@ -2764,7 +2765,10 @@ __device__ __forceinline__ void item_slot(const PtLaunch &lp, long long item, lo
     }
 }
 #ifndef PT_CHUNK
-#define PT_CHUNK 32 /* default (pixel, sample) items a wave takes per dequeue (<= 64) */
+#define PT_CHUNK 64 /* default (pixel, sample) items a wave takes per dequeue (<= 64) */
+#endif
+#ifndef PT_DEQUEUE_PREFETCH
+#define PT_DEQUEUE_PREFETCH 0 /* same-box A/B: C3 -2 %, C5 +-0.5 % (the atomic's wait joins the chunk's first load) */
 #endif
 
 /* The megakernel body.  Persistent: the grid is sized to the resident
@@ -2812,13 +2816,25 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
-    for (;;) {
-        long long chunk = 0;
+    auto dequeue = [&]() {
+        long long c = 0;
         if (lane == 0)
-            chunk = (long long)atomicAdd(work, 1ull);
-        chunk = ((long long)uni((int)(chunk >> 32)) << 32) | (long long)(u32)uni((int)chunk);
+            c = (long long)atomicAdd(work, 1ull);
+        return c;
+    };
+    auto uniform_chunk = [&](long long c) {
+        return ((long long)uni((int)(c >> 32)) << 32) | (long long)(u32)uni((int)c);
+    };
+    long long next = dequeue();
+    for (;;) {
+        const long long chunk = uniform_chunk(next);
         if (chunk >= n_chunks)
             break;
+#if PT_DEQUEUE_PREFETCH
+        /* the next chunk's dequeue is in flight while this one is traced (one
+         * contended device atomic per chunk, ~1-3 us with every wave pulling) */
+        next = dequeue();
+#endif
         const long long item0 = chunk * CH;
         /* the chunk's camera queries, one per lane */
         CamHit ch = {0, 0.0f, 0u, 0};
@@ -2886,6 +2902,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                 ob[3 * j] = c.x, ob[3 * j + 1] = c.y, ob[3 * j + 2] = c.z;
         }
         const V3 mine = mk(ob[3 * lane], ob[3 * lane + 1], ob[3 * lane + 2]);
+#if !PT_DEQUEUE_PREFETCH
+        next = dequeue();
+#endif
         const long long my = item0 + lane;
         if (lp.block_sums) {
             /* the chunk is one 32-sample block of one slot (slot-major, chunk
@@ -2902,9 +2921,12 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                 const float ox = __shfl_down(b.x, w), oy = __shfl_down(b.y, w), oz = __shfl_down(b.z, w);
                 b = mk(b.x + ox, b.y + oy, b.z + oz);
             }
+            /* a 64-item chunk is two blocks: lanes 0-31 and 32-63 (level w <= 16
+             * stays inside each half), lane 32 holds the second partial */
             const float bx = rdlane(b.x, 0), by = rdlane(b.y, 0), bz = rdlane(b.z, 0);
-            const float v = lane == 0 ? bx : lane == 1 ? by : bz;
-            if (lane < 3)
+            const float cx = rdlane(b.x, 32), cy = rdlane(b.y, 32), cz = rdlane(b.z, 32);
+            const float v = lane == 0 ? bx : lane == 1 ? by : lane == 2 ? bz : lane == 3 ? cx : lane == 4 ? cy : cz;
+            if (lane < 3 * (CH >> 5))
                 out[3 * (item0 >> 5) + lane] = v;
         } else if (lane < CH && my < lp.n_items) {
             long long slot;

@@ -550,7 +550,7 @@ size_t stage_floats(const pt_render_params *p, long long npix, long long per_pas
         return (size_t)(npix * per_pass * 3);
     size_t n = (size_t)(npix * (per_pass / 32) * 3);
     n = std::max(n, (size_t)(npix * std::min<long long>(64, p->spp) * 3));
-    n = std::max(n, (size_t)(4ll * 32 * 16384 * 3)); /* a small launch: < 4 chunks of 32 per wave, <= 16384 waves */
+    n = std::max(n, (size_t)(4ll * 64 * 16384 * 3)); /* a small launch: < 4 chunks of 64 per wave, <= 16384 waves */
     return std::min(n, (size_t)(npix * per_pass * 3));
 }
 
@@ -603,14 +603,16 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
         int reduce_mode = 0;
         int nsamp = (int)std::min<long long>(per_pass, p->spp - s0);
         long long n_items = npix * nsamp;
-        /* 32 items per dequeue amortise the queue (A/B on C3: 16 -> 32 +2.7%, 64 same); a launch too small to give
-         * every resident wave a few chunks takes fewer, so one wave does not
-         * trace many samples of one expensive pixel while others idle */
+        /* 64 items per dequeue: every lane of the chunk's camera phase busy
+         * (same-box A/B: C5 2430 -> 4490 Msamples/s, C3 +0.5 %; round 1: C3
+         * 16 -> 32 +2.7 %); a launch too small to give every resident wave a
+         * few chunks takes fewer, so one wave does not trace many samples of
+         * one expensive pixel while others idle */
         const long long waves = (long long)ds.resident_blocks * ds.wpw;
         static const int chunk_max = [] {
             const char *env = getenv("PT_CHUNK_MAX"); /* experiment hook (1..64) */
             if (!env || !*env)
-                return 32;
+                return 64;
             fprintf(stderr, "pt: experiment hook PT_CHUNK_MAX=%s active\n", env);
             return std::max(1, std::min(64, atoi(env)));
         }();
@@ -637,7 +639,8 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
              * (pt_device.h item_slot) */
             lp.sample_major = nsamp <= 64 ? 1 : 0;
             /* one staged partial per 32-sample block when a chunk is a block */
-            lp.block_sums = (block_staging(p) && !lp.sample_major && chunk == 32 && nsamp % 32 == 0) ? 1 : 0;
+            lp.block_sums =
+                (block_staging(p) && !lp.sample_major && (chunk == 32 || chunk == 64) && nsamp % chunk == 0) ? 1 : 0;
             reduce_mode = p->order == PT_ORDER_REFERENCE ? 0 : lp.block_sums ? 2 : 1;
             ds.stage.ensure((size_t)(lp.block_sums ? npix * (nsamp / 32) * 3 : npix * nsamp * 3));
             const float *Pp = ds.P.p;

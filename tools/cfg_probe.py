@@ -16,9 +16,11 @@ name, npix, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 proc = len(sys.argv) > 4 and sys.argv[4] == "procedural"
 disk = [float(v) for v in sys.argv[4].split(":")[1:]] if len(sys.argv) > 4 and sys.argv[4].startswith("disk") else None
 cfg = scenes.CONFIGS[name]
+import dataclasses  # noqa: E402
 if os.environ.get("PROBE_LANE_WALK"):  # A/B of pt_scene_set_lane_walk
-    import dataclasses
     cfg = dataclasses.replace(cfg, lane_walk=int(os.environ["PROBE_LANE_WALK"]))
+if os.environ.get("PROBE_WG"):  # A/B of pt_scene_set_occupancy
+    cfg = dataclasses.replace(cfg, wg_per_cu=int(os.environ["PROBE_WG"]))
 ds = cfg.device_scene(procedural=proc)
 W, H = cfg.width, cfg.height
 rng = np.random.default_rng(1)
