@@ -166,7 +166,7 @@ def main():
     spp = args.spp or cfg.spp
     W, H = cfg.width, cfg.height
     root = cfg.scene()
-    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine, lane_walk=cfg.lane_walk)
+    ds = cfg.device_scene(root=root)
     subset = (SUBSET_1GPU.get(cfg.name, 0) if world == 1 else 0) if args.subset < 0 else args.subset
     keep = None
     if subset:

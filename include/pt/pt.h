@@ -223,6 +223,16 @@ int pt_scene_set_fast_spine(pt_scene *s, int on);
  * bits either way).  Pays where such trees are common (C5's glass ball), costs
  * registers elsewhere.  0 = off.  Takes effect at the next compile/render. */
 int pt_scene_set_lane_walk(pt_scene *s, int frames);
+/* MI355X tuning knob, no reference counterpart: each lane of a chunk walks its
+ * own sample's whole ray tree, scatter loops included, drawing its engine's
+ * numbers one rejection attempt after another; loops of more than 64 children
+ * that mostly end in leaves (a plain diffuse bounce) and fast-order runs of
+ * more than 64 non-zero terms go to the wave as before (same bits either way).
+ * Pays where scatter loops are small or recurse often (C2's
+ * matBrightDiffuseWhite: ~10^4 children, a quarter of them recursing into a
+ * dozen leaves each); supersedes pt_scene_set_lane_walk.  Takes effect at the
+ * next compile/render. */
+int pt_scene_set_lane_scatter(pt_scene *s, int on);
 /* Key of the code object for this scene/depth (hex string, static storage). */
 const char *pt_scene_kernel_key(pt_scene *s, int depth);
 

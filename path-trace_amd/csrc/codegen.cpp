@@ -246,6 +246,9 @@ Generated generate(const SceneImpl &s, int depth)
     /* per-scene lane walk of scatter-free trees (pt_scene_set_lane_walk) */
     if (s.lane_walk > 0)
         src << "#define PT_LANE_WALK " << s.lane_walk << "\n";
+    /* per-scene lane walk with scatter loops (pt_scene_set_lane_scatter) */
+    if (s.lane_scatter)
+        src << "#define PT_LANE_SCATTER 1\n";
     /* experiment hook: A/B a different device library text in the same run,
      * e.g. PT_DEVICE_HEADER=tools/ab/old.h (profiling only) */
     if (const char *hdr = getenv("PT_DEVICE_HEADER")) {

@@ -1612,6 +1612,12 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #ifndef PT_KATT
 #define PT_KATT 8 /* rejection attempts per lane per generation round (A/B on C3: 4 -> 8 +6%) */
 #endif
+#ifndef PT_KATT_SHORT
+#define PT_KATT_SHORT 2 /* per lane, in a short round (a pair of attempts) */
+#endif
+#ifndef PT_SHORT_REM
+#define PT_SHORT_REM 24 /* children left at or below which a round is short (~91 attempts) */
+#endif
 #define PT_RCAP 256  /* kept-child slots per wave awaiting their lane-sum accumulation */
 #define PT_SCAP 128  /* mid / slow queue entries (< 128 pending by construction; byte ring numbers) */
 static_assert(PT_KATT % 2 == 0, "deferred rounds evaluate attempts in pairs");
@@ -1872,6 +1878,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const bool wfin = __builtin_fabsf(rc.x) < 1e37f && __builtin_fabsf(rc.y) < 1e37f && __builtin_fabsf(rc.z) < 1e37f;
     const u64 raw_mask =
         uni_mask((KR0 || length(kR) < 64.0f) && wfin && S::Root::template dark_pre<Emissive<S>>(c0, e));
+    /* children recurse for factor >= eps / (sNa |rc|): short rounds when that
+     * is below 0.99 (over 1 % of the children recurse) */
+    const bool short_nd = !DEFERRED && EPS < 0.99f * (sNa * abs_rc);
     /* queued slots hold ring numbers mod 256; every pending one lies in
      * [keep_sum, keep_sum + PT_RCAP), which restores it */
     auto slot_pos = [&](unsigned char v) { return keep_sum + ((int)(v - keep_sum) & (PT_RCAP - 1)); };
@@ -1895,6 +1904,14 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
              * right after their writes, and only the rare round that stops
              * early needs them again: it evaluates the attempts a second time. */
             int rem = N - (i + npos);
+            /* Short rounds (64 * PT_KATT_SHORT attempts) where a full round
+             * would mostly be thrown away: a burst with few children left (a
+             * recursing child's own small burst), or one whose children often
+             * recurse -- a non-leaf child ends the round, and with factor =
+             * 1 - (1 - cos) sc the child strength (sNa factor) |rc| reaches
+             * eps for factor >= eps / (sNa |rc|) (matBrightDiffuseWhite's
+             * bursts: a quarter of its children) */
+            const int katt = (rem <= PT_SHORT_REM || (!DEFERRED && short_nd)) ? PT_KATT_SHORT : PT_KATT;
             int free_slots = PT_RCAP - (nkeep - keep_sum);
 #ifdef PT_ROOM_CAP
             free_slots = min(free_slots, PT_ROOM_CAP); /* test hook: force early round ends */
@@ -1925,6 +1942,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 u64 sk = lane_state();
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k += 2) {
+                    if (k >= katt)
+                        break;
                     if (k)
                         sk = A64 * sk + g64inc;
                     const u64 sk1 = A64 * sk + g64inc;
@@ -1936,7 +1955,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         if (RAW)
                             D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
                         write_attempt(ap.A[h], ap.A[h] & ~D, h ? sk1 : sk, wn, 0.0f);
-                        if (k + h == PT_KATT - 1)
+                        if (k + h == katt - 1)
                             Alast = ap.A[h], Flast = ap.F[h];
                     }
                     sk = sk1;
@@ -1945,12 +1964,14 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 u64 sk = lane_state();
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k++) {
+                    if (k >= katt)
+                        break;
                     if (k)
                         sk = A64 * sk + g64inc;
                     const Attempt at = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
                     write_attempt(at.A, at.A, sk, at.wn, at.factor);
                     nlor |= at.NL;
-                    if (k == PT_KATT - 1)
+                    if (k == katt - 1)
                         Alast = at.A, Flast = at.F;
                 }
             }
@@ -1960,18 +1981,18 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 #endif
             if (DEFERRED && KR0)
                 PT_MARK(14); /* the diffuse (scatter coefficient 1) variant */
-            int m; /* attempts consumed this round, 1..64*PT_KATT */
+            int m; /* attempts consumed this round, 1..64*katt */
             int np, nk; /* children / kept children consumed */
             /* Common case: the whole round is consumed -- fewer accepted
              * children than remain, no non-leaf child, a slot for every kept
-             * child, and no abort possible (fails <= 487 and at most 512
-             * failures this round) -- so every half takes all its accepted
-             * attempts, and the consecutive-failure count afterwards is that
-             * of the last half, which has an accepted attempt. */
-            if (nlor == 0ull && ta < rem && tk <= free_slots && fails <= 487 && Alast != 0ull) {
+             * child, and no abort possible (fails + the round's 64 katt
+             * attempts stay below 1000) -- so every half takes all its
+             * accepted attempts, and the consecutive-failure count afterwards
+             * is that of the last half, which has an accepted attempt. */
+            if (nlor == 0ull && ta < rem && tk <= free_slots && fails <= 999 - 64 * katt && Alast != 0ull) {
                 const int last = 63 - __builtin_clzll(Alast);
                 fails = (last == 63) ? 0 : __popcll(Flast >> (last + 1));
-                m = 64 * PT_KATT;
+                m = 64 * katt;
                 np = ta;
                 nk = tk;
             } else {
@@ -1997,7 +2018,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 bool cut = false;
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k++) {
-                    if (reason < 0 && !cut) {
+                    if (reason < 0 && !cut && k < katt) {
                         u64 take = 0ull;
                         const int fails_in = fails;
                         const int c = replay(at[k].A, at[k].F, at[k].NL, rem, fails, reason, take);
@@ -2584,6 +2605,276 @@ __device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 d0, const
 }
 #endif
 
+#ifdef PT_LANE_SCATTER
+/* A whole sample walked by its own lane, scatter loops included: the lane
+ * draws its own engine's numbers in the reference's order (path-trace.h:
+ * 138-163, one rejection attempt after another), so every recursing child's
+ * subtree runs where it was generated, with no wave-level spine walk or burst
+ * per child.  This is the shape of matBrightDiffuseWhite's samples (C2): ~10^4
+ * children of which a quarter recurse, each into a dozen leaf children -- a
+ * long chain of small loops that one wave would walk serially (~100 ms per
+ * sample), while 64 lanes walk 64 such samples side by side.
+ *
+ * The fast order's run (oracle.cpp ORDER_FAST) is kept per lane for runs of at
+ * most 64 non-zero terms: each lane sum then holds one term (+0 + t), and the
+ * pairwise tree of the 64 lane sums is formed by a binary counter over the
+ * terms in order, the empty lanes' +0 subtrees folded in at the flush.  A
+ * 65th non-zero term, or a loop of more than 64 children likely to form one
+ * run (a plain diffuse burst: the wave's machinery), gives the sample back to
+ * the wave (returns false; the wave walks it again from its seed).  Pending
+ * nodes live in a per-lane frame array (scratch): one push per recursing
+ * child, the node being shaded stays in registers. */
+struct ScFrame
+{
+    V3 hit, n, a, rc, part, w; /* a: incoming direction (refraction pending) or kR (loop) */
+    float sc, str, add, rf;
+    int dep, N, i, ms;         /* ms: material << 2 | stage */
+};
+enum { LS_AFTER_R = 0, LS_AFTER_M = 1, LS_LOOP = 2 };
+#ifndef PT_LANE_RUN_CAP
+#define PT_LANE_RUN_CAP 64 /* non-zero terms per run a lane keeps (test hook: fewer force hand-backs) */
+#endif
+static_assert(PT_LANE_RUN_CAP <= 64, "a lane's run holds at most one term per lane sum");
+struct Run64
+{
+    V3 s[6], root;
+    int m, len;
+};
+__device__ __forceinline__ void run_reset(Run64 &u) { u.m = 0, u.len = 0; }
+/* adds one term; false on the 65th non-zero term */
+__device__ __forceinline__ bool run_add(Run64 &u, V3 t)
+{
+    u.len++;
+    if (t.x == 0.0f && t.y == 0.0f && t.z == 0.0f)
+        return true;
+    if (u.m == PT_LANE_RUN_CAP)
+        return false;
+    V3 v = mk(0.0f, 0.0f, 0.0f) + t; /* the lane sum: +0 + t */
+    bool stored = false;
+#pragma unroll
+    for (int l = 0; l < 6; l++) {
+        if (!stored) {
+            if ((u.m >> l) & 1)
+                v = u.s[l] + v;
+            else
+                u.s[l] = v, stored = true;
+        }
+    }
+    if (!stored)
+        u.root = v;
+    u.m++;
+    return true;
+}
+/* retval + the pairwise tree of the 64 lane sums (empty run: nothing) */
+__device__ __forceinline__ V3 run_flush(Run64 &u, V3 retval)
+{
+    if (!u.len)
+        return retval;
+    V3 c = mk(0.0f, 0.0f, 0.0f);
+    if (u.m == 64) {
+        c = u.root;
+    } else {
+#pragma unroll
+        for (int l = 0; l < 6; l++)
+            c = ((u.m >> l) & 1) ? u.s[l] + c : c + mk(0.0f, 0.0f, 0.0f);
+    }
+    run_reset(u);
+    return retval + c;
+}
+
+template <class S, int MAXD, bool STRICT>
+__device__ __forceinline__ bool lane_walk_sc(const Env &e, int depth0, V3 d0, const CamHit &ch, Rng rng, V3 &res,
+                                             int &nq, int &nsh)
+{
+    enum { ENTER, SETUP, LOOP, RETURN };
+    ScFrame F[MAXD + 1];
+    ScFrame c; /* the node being shaded */
+    Run64 run;
+    run_reset(run);
+    int sp = 0, state = ENTER;
+    V3 o = mk(0, 0, 0), d = d0, r = mk(0, 0, 0);
+    int dep = depth0;
+    float str = 1.0f;
+    bool first = true;
+    nq = 0, nsh = 0;
+    for (;;) {
+        if (state == ENTER) {
+            nq++;
+            float t = 0.0f;
+            u32 ref = 0;
+            bool ex = false, found;
+            if (first) {
+                found = ch.hit != 0, t = ch.t, ref = ch.ref, ex = ch.ex != 0;
+                first = false;
+            } else {
+                typename S::Root::Ctx ctx;
+                S::Root::prep_l(ctx, o, e);
+                found = lane_first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+            }
+            if (!found) {
+                r = mk(0, 0, 0);
+                state = RETURN;
+                continue;
+            }
+            const V3 hit = o + t * d;
+            const int mat = ref_mat(ref);
+            V3 nn = S::Root::normal(ref_prim(ref), t, o, d, e);
+            if (ref & FLIP)
+                nn = -nn;
+            float ior;
+            V3 n;
+            if (ex) {
+                n = -nn;
+                ior = S::ior(mat, e);
+            } else {
+                n = nn;
+                ior = (float)(1.0 / (double)S::ior(mat, e));
+            }
+            const V3 retval = S::emis(mat, hit, e);
+            if (dep <= 0 || str < EPS) {
+                r = retval;
+                state = RETURN;
+                continue;
+            }
+            nsh++;
+            c.hit = hit, c.n = n, c.a = d, c.part = retval, c.str = str, c.dep = dep, c.add = 1.0f;
+            c.ms = mat << 2;
+            const float rf = clamp01(S::trc(mat, hit, e)) * refract_strength(d, ior, n);
+            c.rf = rf;
+            state = SETUP;
+            if (rf > EPS) {
+                const V3 rd = refract(d, ior, n);
+                if (!is_zero(rd)) {
+                    const V3 tr = S::trans(mat, hit, e);
+                    c.w = (1.0f * rf) * tr; /* addFactor * refractFactor * transmit */
+                    c.ms |= LS_AFTER_R;
+                    F[sp++] = c;
+                    o = hit, d = rd, str = str * rf * 1.0f * length(tr), dep = dep - 1;
+                    state = ENTER;
+                }
+            }
+        } else if (state == SETUP) {
+            if (c.add < EPS) {
+                r = c.part;
+                state = RETURN;
+                continue;
+            }
+            const int mat = c.ms >> 2;
+            const float sc = clamp01(S::scat(mat, c.hit, e));
+            int N = cvt_x86(10000.0f * c.str * c.add * sc);
+            if (sc <= EPS)
+                N = 1;
+            if (N == 0)
+                N = 1;
+            const V3 rc = S::refl(mat, c.hit, e);
+            const V3 refl = reflect(c.a, c.n);
+            if (!(sc > EPS)) { /* one mirror child, added on its own */
+                const float Nf = (float)N;
+                const float factor = 1.0f - (1.0f - dot(refl, c.n)) * sc;
+                c.w = ((c.add / Nf) * factor) * rc;
+                c.ms = (c.ms & ~3) | LS_AFTER_M;
+                F[sp++] = c;
+                o = c.hit, d = refl, str = (((c.str / Nf) * c.add) * factor) * length(rc), dep = c.dep - 1;
+                state = ENTER;
+                continue;
+            }
+            if (N > 64) {
+                /* a loop likely to form a run of more than 64 terms: every
+                 * child is a leaf, or few recurse (factor >= eps / (sNa |rc|)
+                 * with factor = 1 - (1 - cos) sc) */
+                const float sNa = (c.str / (float)N) * c.add, abs_rc = length(rc);
+                const bool all_leaf = c.dep - 1 <= 0 || sNa * abs_rc * 1.01f < EPS;
+                if (all_leaf || (1.0f - EPS / (sNa * abs_rc)) < 0.15f * sc)
+                    return false;
+            }
+            c.a = (1.0f / sc - 1.0f) * refl; /* kR */
+            c.sc = sc, c.rc = rc, c.N = N, c.i = 0;
+            c.ms = (c.ms & ~3) | LS_LOOP;
+            state = LOOP;
+        } else if (state == LOOP) {
+            if (c.i >= c.N) {
+                r = run_flush(run, c.part);
+                state = RETURN;
+                continue;
+            }
+            const float sc = c.sc;
+            const float sNa = (c.str / (float)c.N) * c.add, aN = c.add / (float)c.N, abs_rc = length(c.rc);
+            /* path-trace.h:144-157: rand() redraws outside the unit ball, the
+             * count > 1000 return after 1000 directions in the wrong hemisphere */
+            V3 w;
+            int fails = 0;
+            bool abort = false;
+            for (;;) {
+                const float vx = u11(rng_next(rng)), vy = u11(rng_next(rng)), vz = u11(rng_next(rng));
+                const V3 v = mk(vx, vy, vz);
+                if (dot(v, v) > 0x1.000002p+0f)
+                    continue;
+                w = v + c.a;
+                if (!(dot(c.n, w) <= EPS))
+                    break;
+                if (++fails == 1000) {
+                    abort = true;
+                    break;
+                }
+            }
+            if (abort) {
+                r = run_flush(run, c.part);
+                state = RETURN;
+                continue;
+            }
+            const V3 nd = cnormalize(w);
+            const float factor = 1.0f - (1.0f - dot(nd, c.n)) * sc;
+            const float cs = (sNa * factor) * abs_rc;
+            if (c.dep - 1 <= 0 || cs < EPS) {
+                /* a leaf child: its emission only */
+                nq++;
+                typename S::Root::Ctx ctx;
+                S::Root::prep_l(ctx, c.hit, e);
+                float t = 0.0f;
+                u32 ref = 0;
+                bool ex = false;
+                V3 col = mk(0, 0, 0);
+                if (lane_first_hit<typename S::Root>(ctx, nd, e, t, ref, ex))
+                    col = S::emis(ref_mat(ref), c.hit + t * nd, e);
+                const V3 term = ((aN * factor) * c.rc) * col;
+                if (STRICT)
+                    c.part = c.part + term;
+                else if (!run_add(run, term))
+                    return false;
+                c.i++;
+                continue;
+            }
+            /* a recursing child: the run so far closes, the child's subtree next */
+            if (!STRICT)
+                c.part = run_flush(run, c.part);
+            c.w = (aN * factor) * c.rc;
+            F[sp++] = c;
+            o = c.hit, d = nd, str = cs, dep = c.dep - 1;
+            state = ENTER;
+        } else { /* RETURN */
+            if (sp == 0)
+                break;
+            c = F[--sp];
+            const int stage = c.ms & 3;
+            if (stage == LS_AFTER_R) {
+                c.part = c.part + c.w * r;
+                c.add = 1.0f * (1.0f - c.rf);
+                state = SETUP;
+            } else if (stage == LS_AFTER_M) {
+                r = c.part + c.w * r;
+            } else {
+                c.part = c.part + c.w * r;
+                c.i++;
+                state = LOOP;
+            }
+        }
+    }
+    const V3 z = mk(0, 0, 0);
+    res = (z + r) / 1.0f;
+    return true;
+}
+#endif
+
 template <class S, int MAXD, bool STRICT>
 __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, const WaveLds &L,
                                            const u64 *__restrict__ jump, const u64 *jl, Counters &cnt,
@@ -2857,7 +3148,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             bool ex = false;
             ch.hit = lane_first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
             ch.ex = ex ? 1 : 0;
-#ifdef PT_LANE_WALK /* per scene, pt_scene_set_lane_walk */
+#if defined(PT_LANE_SCATTER) /* per scene, pt_scene_set_lane_scatter */
+            ldone = lane_walk_sc<S, MAXD, STRICT>(e, lp.depth, d, ch, r, lres, lq, lsh) ? 1 : 0;
+#elif defined(PT_LANE_WALK) /* per scene, pt_scene_set_lane_walk */
             ldone = lane_walk<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
 #else
             ldone = lane_sample<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
@@ -2865,7 +3158,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         }
         {
             /* statistics of the samples finished by their lane */
-#ifdef PT_LANE_WALK
+#if defined(PT_LANE_WALK) || defined(PT_LANE_SCATTER)
             {
                 /* per-lane counts: a wave sum of small integers */
                 int q = ldone ? lq : 0, h = ldone ? lsh : 0;

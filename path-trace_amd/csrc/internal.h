@@ -70,6 +70,7 @@ struct SceneImpl
     int wg_per_cu = 0;             /* resident workgroups per CU the kernel is built for (0 = auto) */
     int fast_spine = 0;            /* spine queries try all spans + the fast checks first */
     int lane_walk = 0;             /* register frames of the per-lane scatter-free tree walk (0 = off) */
+    int lane_scatter = 0;          /* per-lane walk of whole trees, scatter loops included */
     std::map<int, std::unique_ptr<DeviceState>> devices;
     std::string last_key;
     void clear()

@@ -1107,6 +1107,14 @@ int pt_scene_set_lane_walk(pt_scene *s, int frames)
     });
 }
 
+int pt_scene_set_lane_scatter(pt_scene *s, int on)
+{
+    return guard([&] {
+        S(s).lane_scatter = on ? 1 : 0;
+        return PT_OK;
+    });
+}
+
 const char *pt_scene_kernel_key(pt_scene *s, int depth)
 {
     thread_local std::string k;

@@ -36,7 +36,8 @@ class DeviceScene:
     """A pt_scene built from a Python scene graph through the C-ABI
     constructors (one pt_* call per reference constructor)."""
 
-    def __init__(self, root: Object, workgroups_per_cu: int = 0, fast_spine: bool = False, lane_walk: int = 0):
+    def __init__(self, root: Object, workgroups_per_cu: int = 0, fast_spine: bool = False, lane_walk: int = 0,
+                 lane_scatter: bool = False):
         L = _lib.lib()
         self._h = L.pt_scene_create()
         if not self._h:
@@ -47,6 +48,8 @@ class DeviceScene:
             _lib.check(L.pt_scene_set_fast_spine(self._h, 1))
         if lane_walk:
             _lib.check(L.pt_scene_set_lane_walk(self._h, int(lane_walk)))
+        if lane_scatter:
+            _lib.check(L.pt_scene_set_lane_scatter(self._h, 1))
         self._img = {}
         self._mat = {}
         self.root = root

@@ -95,6 +95,7 @@ SIGNATURES = {
     "pt_scene_set_occupancy": (_I, [_P, _I]),
     "pt_scene_set_fast_spine": (_I, [_P, _I]),
     "pt_scene_set_lane_walk": (_I, [_P, _I]),
+    "pt_scene_set_lane_scatter": (_I, [_P, _I]),
     "pt_scene_kernel_key": (ctypes.c_char_p, [_P, _I]),
     "pt_selftest_math": (_I, [_I, ctypes.c_uint64, ctypes.c_uint64, _P]),
     "pt_query_spans": (_I, [_P, _I, _P, ctypes.c_int64, _I, _P, _P, _I]),

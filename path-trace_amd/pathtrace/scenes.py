@@ -103,22 +103,21 @@ def procedural_face(size: int, face: int) -> Image:
     return Image(img)
 
 
-def scene_c2(procedural: bool = False):
+def scene_c2(procedural: bool = False, full_mix: bool = True):
     """C2: eight spheres of the demo material mix over a ground plane inside six
     inward sky half-spaces at distance 200 carrying a mirror-ball sky map
     (reference makeSkyMirrorSphere, src/test.cpp:97-100 and :134-140) of
-    test2.hdr (procedural=True: a synthetic 640x480 map, for CPU-only tests)."""
+    test2.hdr (procedural=True: a synthetic 640x480 map, for CPU-only tests).
+    The mix (src/test.cpp:109-118) includes matBrightDiffuseWhite (reflectance
+    8, |rc| = 13.9) on the fourth sphere: the children of a diffuse bounce off
+    it have strength up to 13.9e-4 > eps, so about a quarter of its 10^4
+    children recurse (full_mix=False swaps in plain diffuse, the round-2 C2)."""
     m = materials()
     env = procedural_env(640, 480) if procedural else asset_image("test2.hdr")
     sky = Material(ColorTexture(0), ColorTexture(0),
                    MultiplyTexture((1, 1, 1), MirrorBallSkymapTexture(ImageTexture(env))))
-    # the demo's material mix (src/test.cpp:109-118) minus matBrightDiffuseWhite
-    # (reflectance 8, |rc| = 13.9): the children of a diffuse bounce off it have
-    # strength 13.9e-4 > eps, so none of its 10^4 children is a leaf and each is
-    # a serial walk of its own; measured, the full C2 frame at 2 spp takes
-    # > 150 s on the GPU with it instead of 0.6 s (SURVEY s8(d))
-    mats = [m["diffuse"], m["mirror"], m["glass"], m["diffuse"], m["diamond"], m["mirror"], m["glass"],
-            m["diffuse"]]
+    mats = [m["diffuse"], m["mirror"], m["glass"], m["brightDiffuse"] if full_mix else m["diffuse"], m["diamond"],
+            m["mirror"], m["glass"], m["diffuse"]]
     objs = []
     for k in range(8):
         ang = 2 * math.pi * k / 8
@@ -187,13 +186,16 @@ class Config:
     wg_per_cu: int = 0  # pt_scene_set_occupancy (0 = as many as LDS allows)
     fast_spine: bool = False  # pt_scene_set_fast_spine
     lane_walk: int = 0  # pt_scene_set_lane_walk (register frames; 0 = off)
+    lane_scatter: bool = False  # pt_scene_set_lane_scatter
 
-    def device_scene(self, procedural: bool = False):
-        """The config's scene as a DeviceScene, built at the config's occupancy."""
+    def device_scene(self, procedural: bool = False, root=None):
+        """The config's scene (or `root`) as a DeviceScene with the config's
+        occupancy and walk settings."""
         from . import DeviceScene
-        root = self.scene(procedural=True) if procedural else self.scene()
+        if root is None:
+            root = self.scene(procedural=True) if procedural else self.scene()
         return DeviceScene(root, workgroups_per_cu=self.wg_per_cu, fast_spine=self.fast_spine,
-                           lane_walk=self.lane_walk)
+                           lane_walk=self.lane_walk, lane_scatter=self.lane_scatter)
 
     @property
     def screen(self):
@@ -202,7 +204,10 @@ class Config:
 
 CONFIGS: Dict[str, Config] = {
     "C1": Config("C1", 256, 256, 16, 4, scene_p0, note="plumbing; CPU reference path"),
-    "C2": Config("C2", 1280, 720, 256, 16, scene_c2, note="8 spheres + plane + mirror-ball env (test2.hdr)"),
+    # C2's matBrightDiffuseWhite samples are chains of small recursing loops:
+    # lanes walk them (pt_scene_set_lane_scatter), the wave the plain bursts
+    "C2": Config("C2", 1280, 720, 256, 16, scene_c2, note="8 spheres + plane + mirror-ball env (test2.hdr)",
+                 lane_scatter=True),
     "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG"),
     "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene over 8 GPUs + RCCL framebuffer reduce"),
     # C5 at 2 workgroups per CU: its 14-primitive tree spills 1032 VGPRs at the
@@ -214,3 +219,16 @@ CONFIGS: Dict[str, Config] = {
                  note="demo world + test.hdr spherical env + sky01 skybox", wg_per_cu=2, fast_spine=True,
                  lane_walk=2),
 }
+
+
+def scene_c2_plain(procedural: bool = False):
+    """C2 without matBrightDiffuseWhite (plain diffuse on the fourth sphere):
+    round 2's C2, the scene of tests/golden/config_C2.npz."""
+    return scene_c2(procedural, full_mix=False)
+
+
+# C2 as rounds 1-2 measured it (no recursing scatter children): the config-scale
+# reference fixture and the sampled-pixel GPU tests use it; CONFIGS["C2"] is the
+# reference's full material mix
+C2_PLAIN = Config("C2plain", 1280, 720, 256, 16, scene_c2_plain,
+                  note="8 spheres (no matBrightDiffuseWhite) + plane + mirror-ball env (test2.hdr)")

@@ -34,7 +34,8 @@ def main(names):
     if not O.ref_available():
         sys.exit("needs oracle/_ref/ptref (make -C oracle ref)")
     for name in names:
-        cfg = scenes.CONFIGS[name]
+        # C2: the round-2 scene without matBrightDiffuseWhite (scenes.C2_PLAIN)
+        cfg = scenes.C2_PLAIN if name == "C2" else scenes.CONFIGS[name]
         rng = np.random.default_rng(1000 + int(name[1:]))
         pix = rng.choice(cfg.width * cfg.height, PLAN[name], replace=False)
         if name == "C5":

@@ -143,6 +143,84 @@ def test_lane_walk_c5_same_bits(built):
     assert_bits(imgs[1], imgs[0], "C5 lane walk vs wave walk")
 
 
+# (builder, depth) of the lane scatter walk tests
+LANE_SCATTER_CASES = [("scatter_zoo", 6), ("csg_zoo", 6), ("union_zoo", 6)]
+
+
+@pytest.mark.parametrize("order", ["fast", "reference"])
+@pytest.mark.parametrize("builder,depth", LANE_SCATTER_CASES)
+def test_lane_scatter_bitexact(built, tmp_path, builder, depth, order):
+    """pt_scene_set_lane_scatter: lanes walk whole trees, scatter loops
+    included (their own engine's draws one attempt after another, the fast
+    order's run of <= 64 terms as a binary counter of the pairwise tree): the
+    oracle's bits in both orders.  scatter_zoo has loops of 1..64 children that
+    recurse, a bright diffuse sphere and zero terms among the non-zero ones."""
+    root = T.build(builder)
+    W, H, spp = 48, 32, 2
+    g, st = pt.render(pt.DeviceScene(root, lane_scatter=True), W, H, spp, depth, order=order, stats=True)
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth,
+                 order=O.ORDER_FAST if order == "fast" else O.ORDER_REFERENCE)
+    assert_bits(g, o, "lane scatter, %s %s order vs oracle" % (builder, order))
+    if builder == "scatter_zoo":
+        # lanes finished scatter loops: fewer leaf children went through the wave's
+        # bursts (the dim floor's plain bursts, ~5 000 leaves a sample, stay there)
+        _, st0 = pt.render(pt.DeviceScene(root), W, H, spp, depth, order=order, stats=True)
+        assert st["leaf_queries"] < 0.97 * st0["leaf_queries"], (st["leaf_queries"], st0["leaf_queries"])
+
+
+def test_lane_scatter_run_cap_same_bits(built, tmp_path, monkeypatch):
+    """PT_LANE_RUN_CAP=3 (test hook): a lane hands its sample back to the wave
+    at the 4th non-zero term of a run, mid-walk, after drawing numbers and
+    pushing frames; the wave walks it again from its seed -- the same bits."""
+    monkeypatch.setenv("PT_DEVICE_DEFINES", "PT_LANE_RUN_CAP=3")
+    root = T.scatter_zoo()
+    W, H, spp, depth = 48, 32, 2, 6
+    g = pt.render(pt.DeviceScene(root, lane_scatter=True), W, H, spp, depth, order="fast")
+    o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_FAST)
+    assert_bits(g, o, "lane scatter, run cap 3")
+
+
+def c2_bright_pixels(cfg, n, seed):
+    """hashed pixels plus pixels on the matBrightDiffuseWhite sphere (the
+    fourth sphere, centred near pixel (429, 397) at 1280x720)"""
+    rng = np.random.default_rng(seed)
+    pix = rng.choice(cfg.width * cfg.height, n, replace=False)
+    a, rr = rng.uniform(0, 2 * np.pi, n), 30 * np.sqrt(rng.uniform(0, 1, n))
+    disk = (397 + rr * np.sin(a)).astype(np.int64) * cfg.width + (429 + rr * np.cos(a)).astype(np.int64)
+    return np.unique(np.concatenate([pix, disk])).astype(np.int32)
+
+
+@pytest.mark.parametrize("order", ["fast", "reference"])
+def test_c2_full_mix_bitexact(built, tmp_path, order):
+    """C2 with the reference's full material mix (matBrightDiffuseWhite, src/
+    test.cpp:115) at its depth 16, lanes walking the bright sphere's trees
+    (the config's setting): bright-sphere and hashed pixels bit for bit against
+    the oracle in both orders."""
+    cfg = scenes.CONFIGS["C2"]
+    assert cfg.lane_scatter
+    root = cfg.scene()
+    pix = c2_bright_pixels(cfg, 24, 5)
+    g, st = pt.render(cfg.device_scene(), cfg.width, cfg.height, 1, cfg.depth, screen=cfg.screen, pixels=pix,
+                      order=order, stats=True)
+    o = O.render(to_text(root, str(tmp_path)), cfg.width, cfg.height, 1, cfg.depth, screen=cfg.screen, pixels=pix,
+                 order=O.ORDER_FAST if order == "fast" else O.ORDER_REFERENCE)
+    assert_bits(g, o, "C2 full mix, %s order vs oracle" % order)
+    assert st["queries"] / st["samples"] > 5000  # the bright sphere's samples: ~27 000 queries each
+
+
+def test_c2_lane_scatter_same_bits_as_wave(built):
+    """C2 full mix: the lanes' walk gives the wave walk's bits (4 spp on the
+    bright sphere and hashed pixels)."""
+    cfg = scenes.CONFIGS["C2"]
+    pix = c2_bright_pixels(cfg, 16, 6)
+    imgs = []
+    for ls in (False, True):
+        ds = pt.DeviceScene(cfg.scene(), workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine,
+                            lane_scatter=ls)
+        imgs.append(pt.render(ds, cfg.width, cfg.height, 4, cfg.depth, screen=cfg.screen, pixels=pix))
+    assert_bits(imgs[1], imgs[0], "C2 lane scatter vs wave walk")
+
+
 @pytest.mark.parametrize("builder,depth", [("csg_zoo", 6), ("scene_p1", 8), ("union_zoo", 6)])
 def test_fast_spine_bitexact(built, tmp_path, builder, depth):
     """pt_scene_set_fast_spine: wave-walked queries take every span and the
@@ -160,7 +238,7 @@ def test_full_1080p_frame_on_sampled_pixels(built, tmp_path):
     every pixel; the oracle checks 1500 hashed pixels bit for bit."""
     cfg = scenes.CONFIGS["C3"]
     root = cfg.scene()
-    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine, lane_walk=cfg.lane_walk), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen, stats=True)
+    img, st = pt.render(cfg.device_scene(root=root), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen, stats=True)
     rng = np.random.default_rng(7)
     pix = np.sort(rng.choice(cfg.width * cfg.height, 1500, replace=False)).astype(np.int32)
     o = O.render(to_text(root, str(tmp_path)), cfg.width, cfg.height, 2, cfg.depth, screen=cfg.screen,
@@ -178,7 +256,7 @@ def test_benchmark_configs_on_sampled_pixels(built, tmp_path, name, spp, npix):
     the full frame on the GPU, hashed pixels bit for bit against the oracle."""
     cfg = scenes.CONFIGS[name]
     root = cfg.scene()
-    img, st = pt.render(pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine, lane_walk=cfg.lane_walk), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
+    img, st = pt.render(cfg.device_scene(root=root), cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, stats=True)
     assert st["samples"] == cfg.width * cfg.height * spp
     rng = np.random.default_rng(11)
     pix = np.sort(rng.choice(cfg.width * cfg.height, npix, replace=False)).astype(np.int32)
@@ -279,7 +357,7 @@ def test_c4_eight_shards_on_one_gpu(built, tmp_path):
     (replaces the reference's block farm, src/test.cpp:520-778)."""
     cfg = scenes.CONFIGS["C4"]
     root = cfg.scene()
-    ds = pt.DeviceScene(root, workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine, lane_walk=cfg.lane_walk)
+    ds = cfg.device_scene(root=root)
     W, H, spp = cfg.width, cfg.height, 2
     full = pt.render(ds, W, H, spp, cfg.depth, screen=cfg.screen).reshape(-1, 3)
     acc = np.zeros_like(full)
@@ -354,7 +432,9 @@ def test_config_scale_vs_reference(built, name, tmp_path):
     z = np.load(os.path.join(GOLD, "config_%s.npz" % name))
     pix, ref = z["pixels"], z["means"]
     W, H, spp, depth, seed = [int(v) for v in z["meta"][:5]]
-    cfg = scenes.CONFIGS[name]
+    # config_C2.npz holds C2 without matBrightDiffuseWhite (scenes.C2_PLAIN); the
+    # full mix is checked against the oracle (test_c2_full_mix_bitexact)
+    cfg = scenes.C2_PLAIN if name == "C2" else scenes.CONFIGS[name]
     ds = cfg.device_scene()
     g = pt.render(ds, W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix, order="reference")
     if name == "C5":

@@ -145,6 +145,30 @@ def union_zoo():
     return union_array(objs)
 
 
+def scatter_zoo():
+    """Scatter loops a lane walks whole (pt_scene_set_lane_scatter): small
+    glossy loops (N = 10^4 strength sc <= 64 children, which recurse), a bright
+    diffuse sphere whose children recurse in part (matBrightDiffuseWhite's
+    reflectance 8), a dim diffuse floor (a plain burst: the wave's), glass and a
+    mirror, under a sky whose upper wall emits nothing (zero terms among the
+    non-zero ones)."""
+    tiny = Material(ColorTexture(0.9, 0.8, 0.7), ColorTexture(0.0064))
+    small = Material(ColorTexture(0.6), ColorTexture(0.002))
+    bright = Material(ColorTexture(8), ColorTexture(1))
+    dim = Material(ColorTexture(0.3, 0.25, 0.2), ColorTexture(1))
+    glass = Material(ColorTexture(0.7), ColorTexture(0), ColorTexture(0), ColorTexture(0.9, 0.95, 1.0), 1.45,
+                     ColorTexture(0.8))
+    mirror = Material(ColorTexture(0.99), ColorTexture(0))
+    emit = Material(ColorTexture(0), ColorTexture(0), ColorTexture(1.5, 1.2, 0.9))
+    sky = Material(ColorTexture(0), ColorTexture(0), ColorTexture(0.4, 0.6, 1.0))
+    black = Material(ColorTexture(0), ColorTexture(0), ColorTexture(0))
+    return union_array([
+        Sphere((-1.0, 0.0, -4.0), 0.6, tiny), Sphere((0.3, -0.3, -3.6), 0.35, bright),
+        Sphere((1.1, 0.1, -4.2), 0.55, small), Sphere((-0.2, 0.7, -4.8), 0.5, glass),
+        Sphere((0.9, 0.9, -5.0), 0.4, mirror), Sphere((-1.2, 1.0, -5.5), 0.3, emit),
+        Plane((0, 1, 0), 0.7, dim), Plane((0, -1, 0), 3.0, black), Plane((0, 0, 1), 30, sky)])
+
+
 def texture_points(n=2048, seed=13):
     """Lookup points for the texture query goldens (pt_tex_eval): random points
     in a box, unit directions (the sky maps' domain), points on the cube-face

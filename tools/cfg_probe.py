@@ -21,6 +21,11 @@ if os.environ.get("PROBE_LANE_WALK"):  # A/B of pt_scene_set_lane_walk
     cfg = dataclasses.replace(cfg, lane_walk=int(os.environ["PROBE_LANE_WALK"]))
 if os.environ.get("PROBE_WG"):  # A/B of pt_scene_set_occupancy
     cfg = dataclasses.replace(cfg, wg_per_cu=int(os.environ["PROBE_WG"]))
+if os.environ.get("PROBE_C2_PLAIN"):  # C2 without matBrightDiffuseWhite (round 2's C2)
+    from pathtrace.scenes import scene_c2
+    cfg = dataclasses.replace(cfg, scene=lambda procedural=False: scene_c2(procedural, full_mix=False))
+if os.environ.get("PROBE_FAST_SPINE"):
+    cfg = dataclasses.replace(cfg, fast_spine=bool(int(os.environ["PROBE_FAST_SPINE"])))
 ds = cfg.device_scene(procedural=proc)
 W, H = cfg.width, cfg.height
 rng = np.random.default_rng(1)

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-3 evidence: per config, the bench's rocprofv3 kernel-trace summary and
+# its PMC passes (issue/busy counters, FETCH_SIZE, WRITE_SIZE); then the
+# adaptive caller vs the full frame at C3 16 spp.
+# usage: tools/r3_evidence.sh OUTDIR [configs...]
+OUT=${1:-gpurun_out/r3ev}; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$OUT"; OUT=$(cd "$OUT" && pwd)
+CFGS=("$@"); [ ${#CFGS[@]} -gt 0 ] || CFGS=(C3 C5)
+for c in "${CFGS[@]}"; do
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$c" -o bench --output-format csv -- python3 "$ROOT/bench.py" --config $c --no-cpu > "$OUT/prof_$c.json" 2> "$OUT/prof_$c.err")
+  rc=$?; echo "prof $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  bash "$ROOT/tools/pmc_bench.sh" "$OUT/pmc_$c" --config $c
+  rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+timeout -k 10 600 python3 "$ROOT/tools/probe_adaptive.py" C3 16 > "$OUT/adaptive_c3_16spp.json" 2>&1
+rc=$?; echo "adaptive rc=$rc"; exit $rc
