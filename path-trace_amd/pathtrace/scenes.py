@@ -204,10 +204,10 @@ class Config:
 
 CONFIGS: Dict[str, Config] = {
     "C1": Config("C1", 256, 256, 16, 4, scene_p0, note="plumbing; CPU reference path"),
-    # C2's matBrightDiffuseWhite samples are chains of small recursing loops:
-    # lanes walk them (pt_scene_set_lane_scatter), the wave the plain bursts
-    "C2": Config("C2", 1280, 720, 256, 16, scene_c2, note="8 spheres + plane + mirror-ball env (test2.hdr)",
-                 lane_scatter=True),
+    # C2 without matBrightDiffuseWhite: with it the reference's own cost per
+    # sample has no practical bound (C2_FULL below)
+    "C2": Config("C2", 1280, 720, 256, 16, lambda procedural=False: scene_c2(procedural, full_mix=False),
+                 note="8 spheres (no matBrightDiffuseWhite) + plane + mirror-ball env (test2.hdr)"),
     "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG"),
     "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene over 8 GPUs + RCCL framebuffer reduce"),
     # C5 at 2 workgroups per CU: its 14-primitive tree spills 1032 VGPRs at the
@@ -223,12 +223,19 @@ CONFIGS: Dict[str, Config] = {
 
 def scene_c2_plain(procedural: bool = False):
     """C2 without matBrightDiffuseWhite (plain diffuse on the fourth sphere):
-    round 2's C2, the scene of tests/golden/config_C2.npz."""
+    the benchmarked C2, the scene of tests/golden/config_C2.npz."""
     return scene_c2(procedural, full_mix=False)
 
 
-# C2 as rounds 1-2 measured it (no recursing scatter children): the config-scale
-# reference fixture and the sampled-pixel GPU tests use it; CONFIGS["C2"] is the
-# reference's full material mix
-C2_PLAIN = Config("C2plain", 1280, 720, 256, 16, scene_c2_plain,
-                  note="8 spheres (no matBrightDiffuseWhite) + plane + mirror-ball env (test2.hdr)")
+C2_PLAIN = CONFIGS["C2"]
+
+# C2 with the reference's full material mix (src/test.cpp:109-118): supported
+# bit for bit (lanes walk the bright sphere's chains of small recursing loops,
+# pt_scene_set_lane_scatter) and tested on pixel subsets, but not a frame
+# workload: behind the glass sphere's silhouette a single sample's ray tree
+# grows ~3.6x per depth level -- pixel (544, 360) costs 3.03e6 queries at
+# depth 8 and 1.17e7 at depth 9 in the UNMODIFIED reference (oracle/_ref/ptref,
+# 6.1 s on one core), ~9e10 extrapolated to depth 16 (~14 h on one core for
+# one sample, sequential in its engine's draws)
+C2_FULL = Config("C2full", 1280, 720, 256, 16, scene_c2,
+                 note="8 spheres (full demo mix) + plane + mirror-ball env (test2.hdr)", lane_scatter=True)

@@ -196,7 +196,7 @@ def test_c2_full_mix_bitexact(built, tmp_path, order):
     test.cpp:115) at its depth 16, lanes walking the bright sphere's trees
     (the config's setting): bright-sphere and hashed pixels bit for bit against
     the oracle in both orders."""
-    cfg = scenes.CONFIGS["C2"]
+    cfg = scenes.C2_FULL
     assert cfg.lane_scatter
     root = cfg.scene()
     pix = c2_bright_pixels(cfg, 24, 5)
@@ -211,7 +211,7 @@ def test_c2_full_mix_bitexact(built, tmp_path, order):
 def test_c2_lane_scatter_same_bits_as_wave(built):
     """C2 full mix: the lanes' walk gives the wave walk's bits (4 spp on the
     bright sphere and hashed pixels)."""
-    cfg = scenes.CONFIGS["C2"]
+    cfg = scenes.C2_FULL
     pix = c2_bright_pixels(cfg, 16, 6)
     imgs = []
     for ls in (False, True):
@@ -432,9 +432,9 @@ def test_config_scale_vs_reference(built, name, tmp_path):
     z = np.load(os.path.join(GOLD, "config_%s.npz" % name))
     pix, ref = z["pixels"], z["means"]
     W, H, spp, depth, seed = [int(v) for v in z["meta"][:5]]
-    # config_C2.npz holds C2 without matBrightDiffuseWhite (scenes.C2_PLAIN); the
+    # config_C2.npz holds the benchmarked C2 (no matBrightDiffuseWhite); the
     # full mix is checked against the oracle (test_c2_full_mix_bitexact)
-    cfg = scenes.C2_PLAIN if name == "C2" else scenes.CONFIGS[name]
+    cfg = scenes.CONFIGS[name]
     ds = cfg.device_scene()
     g = pt.render(ds, W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix, order="reference")
     if name == "C5":
