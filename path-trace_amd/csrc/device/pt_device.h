@@ -1613,7 +1613,10 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 #define PT_KATT 8 /* rejection attempts per lane per generation round (A/B on C3: 4 -> 8 +6%) */
 #endif
 #ifndef PT_KATT_SHORT
-#define PT_KATT_SHORT 2 /* per lane, in a short round (a pair of attempts) */
+/* per lane, in a short round; off (= PT_KATT) by default: short rounds of 2
+ * cost C3 6 % (same-box A/B 143.4 vs 152.0 Msamples/s at 256 spp), and the
+ * bursts they were for (matBrightDiffuseWhite's) are walked by lanes */
+#define PT_KATT_SHORT PT_KATT
 #endif
 #ifndef PT_SHORT_REM
 #define PT_SHORT_REM 24 /* children left at or below which a round is short (~91 attempts) */

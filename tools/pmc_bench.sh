@@ -1,7 +1,9 @@
 #!/bin/bash
-# Counter evidence for the bench line: three rocprofv3 --pmc passes of the
-# bench command itself (issue/busy counters, FETCH_SIZE, WRITE_SIZE -- never
-# combined with tracing), summarised by tools/pmc_summary.py into OUT/pmc.json.
+# Counter evidence for the bench line: rocprofv3 --pmc passes of the bench
+# command itself (never combined with tracing; one counter group per pass),
+# summarised by tools/pmc_summary.py into OUT/pmc.json.
+#   busy   issue/busy counters        fetch  FETCH_SIZE     write  WRITE_SIZE
+#   stall  wave-cycle split + memory instruction mix     cache  L2 hits/misses
 # usage: tools/pmc_bench.sh OUTDIR [bench args...]
 OUT=${1:-gpurun_out/pmcb}; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -17,4 +19,6 @@ BENCH_ARGS=("$@")
 pass busy SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
+pass stall SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_FLAT SQ_INSTS_LDS SQ_INSTS_SMEM
+pass cache TCC_HIT_sum TCC_MISS_sum
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/pmc.json" && cat "$OUT/pmc.json"

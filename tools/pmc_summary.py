@@ -36,6 +36,7 @@ def bench_line(name):
 
 
 busy, fetch, write = counters("busy"), counters("fetch"), counters("write")
+stall, cache = counters("stall"), counters("cache")
 b = bench_line("busy")
 launches = b["steps"]  # one render launch per step at the bench config (one pass)
 samples = b["value"] * 1e6 * b["ms_per_step"] * 1e-3 * b["steps"]
@@ -56,6 +57,16 @@ res = {
     "fetch_bytes_per_launch": 2 * 1024 * fetch["FETCH_SIZE"] / launches,
     "write_bytes_per_launch": 1024 * write["WRITE_SIZE"] / launches,
 }
+if stall:
+    wc = stall["SQ_WAVE_CYCLES"]
+    # disjoint buckets of a wave's life (MI355X_MICROARCH.md, PMC slots)
+    res["wave_cycle_split"] = {"waiting (s_waitcnt/barrier)": stall["SQ_WAIT_ANY"] / wc,
+                               "issue-stalled": stall["SQ_WAIT_INST_ANY"] / wc,
+                               "issuing": stall["SQ_ACTIVE_INST_ANY"] / wc}
+    for k in ("SQ_INSTS_VMEM_RD", "SQ_INSTS_FLAT", "SQ_INSTS_LDS", "SQ_INSTS_SMEM"):
+        res[k.lower()[9:] + "_insts_per_sample"] = stall[k] / samples
+if cache:
+    res["l2_hit_rate"] = cache["TCC_HIT_sum"] / max(1.0, cache["TCC_HIT_sum"] + cache["TCC_MISS_sum"])
 res["hbm_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
 res["hbm_bytes_per_sample"] = res["hbm_bytes_per_launch"] * launches / samples
 if kernel_s:

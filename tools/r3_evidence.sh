@@ -1,7 +1,6 @@
 #!/bin/bash
 # Round-3 evidence: per config, the bench's rocprofv3 kernel-trace summary and
-# its PMC passes (issue/busy counters, FETCH_SIZE, WRITE_SIZE); then the
-# adaptive caller vs the full frame at C3 16 spp.
+# its PMC passes (tools/pmc_bench.sh), each step under its own limit.
 # usage: tools/r3_evidence.sh OUTDIR [configs...]
 OUT=${1:-gpurun_out/r3ev}; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -13,5 +12,3 @@ for c in "${CFGS[@]}"; do
   bash "$ROOT/tools/pmc_bench.sh" "$OUT/pmc_$c" --config $c
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
-timeout -k 10 600 python3 "$ROOT/tools/probe_adaptive.py" C3 16 > "$OUT/adaptive_c3_16spp.json" 2>&1
-rc=$?; echo "adaptive rc=$rc"; exit $rc
