@@ -42,7 +42,7 @@ VALU_PEAK_TOPS = 78.6  # 256 CU x 128 FP32 lanes/clk x 2.4 GHz, no FMA (contract
 OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 614.78, "C5": 554.13}
 # Counter evidence of this same command (tools/pmc_bench.sh: rocprofv3 --pmc
 # passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 + WRITE_SIZE)
-PMC_JSON = os.path.join(ROOT, "profiles", "round2", "pmc_bench_%s.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "round3", "pmc_bench_%s.json")
 # bounded CPU samples at full spp on the box's per-GPU CPU share (16 threads):
 # BASELINE.md's 4096 hashed pixels (C3: ~60 s), fewer where a pixel costs more
 CPU_PIXELS = {"C1": 4096, "C2": 512, "C3": 4096, "C4": 1024, "C5": 32768}
@@ -238,7 +238,8 @@ def main():
         if opq:
             ops_per_launch = opq * queries / (args.steps * launches_per_step * world)
             achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12
-            ev = pmc_evidence(cfg.name) if (not subset and spp == cfg.spp) else None
+            # the PMC passes ran this same command at N = 1 (config defaults: C5's subset)
+            ev = pmc_evidence(cfg.name) if (world == 1 and args.subset < 0 and not args.spp) else None
             out["roofline"] = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS,
                                "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
                                "traffic": round(ev["hbm_bytes_per_launch"]) if ev else None,

@@ -4,6 +4,7 @@
 # summarised by tools/pmc_summary.py into OUT/pmc.json.
 #   busy   issue/busy counters        fetch  FETCH_SIZE     write  WRITE_SIZE
 #   stall  wave-cycle split + memory instruction mix     cache  L2 hits/misses
+#   tex    texture address/data unit busy (TA, TD) and flat read wavefronts
 # usage: tools/pmc_bench.sh OUTDIR [bench args...]
 OUT=${1:-gpurun_out/pmcb}; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -21,4 +22,5 @@ pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 pass stall SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_FLAT SQ_INSTS_LDS SQ_INSTS_SMEM
 pass cache TCC_HIT_sum TCC_MISS_sum
+pass tex TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/pmc.json" && cat "$OUT/pmc.json"

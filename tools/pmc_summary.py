@@ -36,7 +36,7 @@ def bench_line(name):
 
 
 busy, fetch, write = counters("busy"), counters("fetch"), counters("write")
-stall, cache = counters("stall"), counters("cache")
+stall, cache, tex = counters("stall"), counters("cache"), counters("tex")
 b = bench_line("busy")
 launches = b["steps"]  # one render launch per step at the bench config (one pass)
 samples = b["value"] * 1e6 * b["ms_per_step"] * 1e-3 * b["steps"]
@@ -67,6 +67,12 @@ if stall:
         res[k.lower()[9:] + "_insts_per_sample"] = stall[k] / samples
 if cache:
     res["l2_hit_rate"] = cache["TCC_HIT_sum"] / max(1.0, cache["TCC_HIT_sum"] + cache["TCC_MISS_sum"])
+if tex:
+    tgui = tex["GRBM_GUI_ACTIVE"] / XCDS
+    # one TA and one TD per CU (256): busy cycles over the kernel's active cycles
+    res["ta_busy"] = tex["TA_TA_BUSY_sum"] / 256 / tgui
+    res["td_busy"] = tex["TD_TD_BUSY_sum"] / 256 / tgui
+    res["flat_read_wavefronts_per_sample"] = tex["TA_FLAT_READ_WAVEFRONTS_sum"] / samples
 res["hbm_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
 res["hbm_bytes_per_sample"] = res["hbm_bytes_per_launch"] * launches / samples
 if kernel_s:
