@@ -76,6 +76,8 @@ struct PtLaunch
     int block_sums;     /* stage one partial per 32-sample block (slot-major,
                            chunk 32 or 64, nsamp % chunk == 0), else one value
                            per sample */
+    long long perm;     /* sample-major: slot = (k * perm) mod nslots for the k-th
+                           slot of a sample (perm coprime to nslots; 0 = k)      */
 };
 
 struct Env
@@ -3052,6 +3054,11 @@ __device__ __forceinline__ void item_slot(const PtLaunch &lp, long long item, lo
         const long long nslots = lp.n_items / lp.nsamp;
         const long long k = item / nslots;
         slot = item - k * nslots;
+        /* a chunk's slots spread over the pixel list: the expensive pixels of
+         * a small launch (a mirror's reflection, clustered in the list) do not
+         * fall into one wave's chunk, which it would walk one by one */
+        if (lp.perm)
+            slot = (long long)(((unsigned long long)slot * (unsigned long long)lp.perm) % (unsigned long long)nslots);
         s = lp.s0 + (int)k;
     } else {
         slot = item / lp.nsamp;
@@ -3093,6 +3100,22 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const u64 t_start = __builtin_amdgcn_s_memrealtime(); /* 100 MHz: wave lifetimes, stats[26..29] */
     const Env e = {P, imgs};
+#ifdef PT_POISON_LDS
+    /* test build: every LDS word starts as all-ones (NaN floats, ring numbers
+     * 255, -1 integers) instead of whatever the CU's previous workgroup left,
+     * so a read of LDS state this launch has not written changes the bits
+     * (round 2's kept-only position flags read stale flags in small launches) */
+    {
+        auto poison = [&](void *p, unsigned bytes) {
+            for (unsigned k = threadIdx.x; k < bytes / 4; k += blockDim.x)
+                ((u32 *)p)[k] = 0xFFFFFFFFu;
+        };
+        poison(stk, sizeof stk), poison(xbuf, sizeof xbuf), poison(rbuf, sizeof rbuf), poison(sbuf, sizeof sbuf);
+        poison(mbuf, sizeof mbuf), poison(cbuf, sizeof cbuf), poison(lbuf, sizeof lbuf), poison(obuf, sizeof obuf);
+        poison(jbuf, sizeof jbuf);
+        __syncthreads();
+    }
+#endif
     if (wave == 0)
         jbuf[lane][0] = jump[2 * lane], jbuf[lane][1] = jump[2 * lane + 1];
     __syncthreads();

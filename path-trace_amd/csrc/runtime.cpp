@@ -72,6 +72,7 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     int gw, chunk;
     int sample_major;
     int block_sums;
+    long long perm;
 };
 
 template <class T>
@@ -540,6 +541,36 @@ long long pass_samples(const pt_render_params *p, long long npix)
     return per_pass;
 }
 
+/* Multiplier of the sample-major slot permutation (pt_device.h item_slot): a
+ * prime near nslots / phi that does not divide nslots, so consecutive slots
+ * of a chunk land ~0.38 of the list apart; 0 (identity) below 128 slots or
+ * with PT_SAMPLE_PERM=0 (experiment hook). */
+long long slot_permutation(long long nslots)
+{
+    static const bool on = [] {
+        const char *env = getenv("PT_SAMPLE_PERM");
+        if (env && *env == '0') {
+            fprintf(stderr, "pt: experiment hook PT_SAMPLE_PERM=0 active\n");
+            return false;
+        }
+        return true;
+    }();
+    if (!on || nslots < 128)
+        return 0;
+    auto prime = [](long long v) {
+        if (v < 2)
+            return false;
+        for (long long d = 2; d * d <= v; d++)
+            if (v % d == 0)
+                return false;
+        return true;
+    };
+    for (long long m = (long long)((double)nslots * 0.6180339887) | 1; m > 2; m -= 2)
+        if (prime(m) && nslots % m != 0)
+            return m;
+    return 0;
+}
+
 /* Stage floats for the largest launch of a render: block partials for
  * slot-major whole-block launches, else one value per sample -- launches of
  * <= 64 samples per slot (sample-major) and small launches whose chunks fall
@@ -638,6 +669,8 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             /* sample-major item order for launches of up to 64 samples per slot
              * (pt_device.h item_slot) */
             lp.sample_major = nsamp <= 64 ? 1 : 0;
+            if (lp.sample_major)
+                lp.perm = slot_permutation(npix);
             /* one staged partial per 32-sample block when a chunk is a block */
             lp.block_sums =
                 (block_staging(p) && !lp.sample_major && (chunk == 32 || chunk == 64) && nsamp % chunk == 0) ? 1 : 0;

@@ -143,6 +143,9 @@ def test_lane_walk_c5_same_bits(built):
     assert_bits(imgs[1], imgs[0], "C5 lane walk vs wave walk")
 
 
+# (builder, depth) of the poisoned-LDS test build (test_lds_poison_bitexact)
+POISON_CASES = [("scene_p1", 8), ("csg_zoo", 6)]
+
 # (builder, depth) of the lane scatter walk tests
 LANE_SCATTER_CASES = [("scatter_zoo", 6), ("csg_zoo", 6), ("union_zoo", 6)]
 
@@ -346,6 +349,30 @@ def test_round_cut_paths_bitexact(built, tmp_path, monkeypatch, cap):
     g = pt.render(root, W, H, spp, depth)
     o = O.render(to_text(root, str(tmp_path)), W, H, spp, depth, order=O.ORDER_FAST)
     assert_bits(g, o, "PT_ROOM_CAP=%d" % cap)
+
+
+@pytest.mark.parametrize("builder,depth", POISON_CASES)
+def test_lds_poison_bitexact(built, tmp_path, monkeypatch, builder, depth):
+    """PT_POISON_LDS (test build): every LDS word starts all-ones, so any read
+    of LDS state the launch has not written (round 2's j3 failure: kept-only
+    position flags read stale flags left by an earlier launch or by a round's
+    speculative writes) changes the bits.  Small pixel-list launches -- the
+    adaptive caller's shape -- with forced early round ends (PT_ROOM_CAP=3)
+    and whole frames, fast and reference order, against the oracle."""
+    monkeypatch.setenv("PT_DEVICE_DEFINES", "PT_POISON_LDS=1 PT_ROOM_CAP=3")
+    root = T.build(builder)
+    txt = to_text(root, str(tmp_path))
+    W, H = 40, 28
+    rng = np.random.default_rng(3)
+    ds = pt.DeviceScene(root)
+    for order, oo in (("fast", O.ORDER_FAST), ("reference", O.ORDER_REFERENCE)):
+        g = pt.render(ds, W, H, 3, depth, order=order)
+        assert_bits(g, O.render(txt, W, H, 3, depth, order=oo), "poisoned LDS, %s frame" % order)
+        for n in (1, 7, 70):  # launches far smaller than the grid
+            pix = np.sort(rng.choice(W * H, n, replace=False)).astype(np.int32)
+            g = pt.render(ds, W, H, 5, depth, pixels=pix, order=order)
+            assert_bits(g, O.render(txt, W, H, 5, depth, pixels=pix, order=oo),
+                        "poisoned LDS, %s, %d pixels" % (order, n))
 
 
 def test_c4_eight_shards_on_one_gpu(built, tmp_path):
