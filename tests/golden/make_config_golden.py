@@ -27,15 +27,15 @@ from pathtrace.scene import to_text  # noqa: E402
 
 SEED = 0x5EED
 # hashed pixels per config (full spp, full depth); sized for minutes on 8 cores
-PLAN = {"C3": 1024, "C2": 256, "C5": 48}
+PLAN = {"C3": 1024, "C2": 256, "C5": 512}
 
 
 def main(names):
     if not O.ref_available():
         sys.exit("needs oracle/_ref/ptref (make -C oracle ref)")
     for name in names:
-        # C2: the round-2 scene without matBrightDiffuseWhite (scenes.C2_PLAIN)
-        cfg = scenes.C2_PLAIN if name == "C2" else scenes.CONFIGS[name]
+        # C2: the benchmarked scene, without matBrightDiffuseWhite
+        cfg = scenes.CONFIGS[name]
         rng = np.random.default_rng(1000 + int(name[1:]))
         pix = rng.choice(cfg.width * cfg.height, PLAN[name], replace=False)
         if name == "C5":
@@ -44,11 +44,15 @@ def main(names):
             # inside EPS: the demo's spheres and lens at z ~ -4 vanish and the
             # frame is the test.hdr sky box plus the sky01 skybox sphere at
             # (0, 1.2, -6), r 0.7 (projected centre (1920, 648), radius ~250
-            # px).  Half the pixels are drawn on that sphere.
-            pix = pix[:PLAN[name] // 2]
-            ang, rad = rng.uniform(0, 2 * np.pi, PLAN[name] // 2), 200 * np.sqrt(rng.uniform(0, 1, PLAN[name] // 2))
-            xs, ys = np.floor(1920 + rad * np.cos(ang)), np.floor(648 + rad * np.sin(ang))
-            pix = np.concatenate([pix, (ys * cfg.width + xs).astype(np.int64)])
+            # px).  A quarter of the pixels are drawn on that sphere and a
+            # quarter on the far side of the glass ball (centre (2460, 1080),
+            # radius ~400 px: refraction and mirror chains, ~60x a sky pixel).
+            q = PLAN[name] // 4
+            pix = pix[:2 * q]
+            for cx, cy, r in ((1920, 648, 200), (2460, 1080, 400)):
+                ang, rad = rng.uniform(0, 2 * np.pi, q), r * np.sqrt(rng.uniform(0, 1, q))
+                xs, ys = np.floor(cx + rad * np.cos(ang)), np.floor(cy + rad * np.sin(ang))
+                pix = np.concatenate([pix, (ys * cfg.width + xs).astype(np.int64)])
         pix = np.unique(pix).astype(np.int32)
         txt = to_text(cfg.scene(), "/tmp/pt_cfg_golden_%s" % name)
         t = time.time()

@@ -94,3 +94,20 @@ def test_pixel_mean_is_sequential_sum(built, tmp_path):
     for s in range(spp):
         acc = (acc + ps[:, s]).astype(np.float32)
     np.testing.assert_array_equal(mean, (acc / np.float32(spp)).astype(np.float32))
+
+
+@pytest.mark.parametrize("name,npix", [("C5", 0), ("C2", 24)])
+def test_config_golden_matches_oracle(built, tmp_path, name, npix):
+    """The config-scale fixtures of the unmodified reference (config_*.npz,
+    make_config_golden.py) against the oracle's reference order at the
+    config's full spp and depth, bit for bit: C5's 512 pixels (hashed, skybox
+    sphere, glass ball) whole, C2 on its first npix pixels (CPU time)."""
+    z = load("config_%s.npz" % name)
+    pix, ref = z["pixels"], z["means"]
+    if npix:
+        pix, ref = pix[:npix], ref[:npix]
+    W, H, spp, depth, seed = [int(v) for v in z["meta"][:5]]
+    cfg = scenes.CONFIGS[name]
+    assert (W, H, spp, depth) == (cfg.width, cfg.height, cfg.spp, cfg.depth)
+    got = O.render(to_text(cfg.scene(), str(tmp_path)), W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix)
+    np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
