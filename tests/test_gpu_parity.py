@@ -300,6 +300,24 @@ def test_edge_shapes_and_depths(built, tmp_path, W, H, spp, depth):
     assert_bits(g, o, "edge %dx%d spp %d depth %d" % (W, H, spp, depth))
 
 
+@pytest.mark.parametrize("npix", [127, 128, 210, 2310, 4096])
+def test_sample_major_slot_permutation(built, tmp_path, npix):
+    """Launches of <= 64 samples per pixel take their slots in a multiplicative
+    permutation (runtime.cpp slot_permutation: a prime near n/phi that does not
+    divide n; none below 128 slots).  Pixel-list sizes around the threshold
+    and with many small prime factors (210, 2310): every slot rendered once,
+    the oracle's bits in both orders."""
+    root = T.csg_zoo()
+    W, H = 80, 60
+    pix = np.sort(np.random.default_rng(npix).choice(W * H, npix, replace=False)).astype(np.int32)
+    txt = to_text(root, str(tmp_path))
+    ds = pt.DeviceScene(root)
+    for order, oo in (("fast", O.ORDER_FAST), ("reference", O.ORDER_REFERENCE)):
+        g, st = pt.render(ds, W, H, 3, 6, pixels=pix, order=order, stats=True)
+        assert st["samples"] == npix * 3
+        assert_bits(g, O.render(txt, W, H, 3, 6, pixels=pix, order=oo), "%d slots, %s" % (npix, order))
+
+
 def test_empty_pixel_list(built):
     out = pt.render(scenes.scene_p0(), 8, 8, 2, 4, pixels=np.zeros(0, dtype=np.int32))
     assert out.shape == (0, 3)
