@@ -208,8 +208,12 @@ CONFIGS: Dict[str, Config] = {
     # sample has no practical bound (C2_FULL below)
     "C2": Config("C2", 1280, 720, 256, 16, lambda procedural=False: scene_c2(procedural, full_mix=False),
                  note="8 spheres (no matBrightDiffuseWhite) + plane + mirror-ball env (test2.hdr)"),
-    "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG"),
-    "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene over 8 GPUs + RCCL framebuffer reduce"),
+    # C3/C4: span-first spine queries (same-box A/B at 1024 spp: 156.3 -> 157.2
+    # Msamples/s; round 2's kernel lost 0.9 % with them)
+    "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG",
+                 fast_spine=True),
+    "C4": Config("C4", 1920, 1080, 4096, 8, scene_p1, gpus=8, note="C3 scene over 8 GPUs + RCCL framebuffer reduce",
+                 fast_spine=True),
     # C5 at 2 workgroups per CU: its 14-primitive tree spills 1032 VGPRs at the
     # default cap of 128 (119 -> 277 Msamples/s on one MI355X, round 2).  Its
     # glass-ball trees have no scatter loop: lanes walk them with 2 register

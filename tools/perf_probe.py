@@ -11,7 +11,7 @@ from pathtrace import scenes  # noqa: E402
 
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 order = sys.argv[2] if len(sys.argv) > 2 else "fast"
-ds = pt.DeviceScene(scenes.scene_p1())
+ds = scenes.CONFIGS["C3"].device_scene()  # the bench config's scene and settings
 t = time.time()
 img, st = pt.render(ds, 1920, 1080, spp, 8, stats=True, order=order)
 dt = time.time() - t
