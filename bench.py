@@ -238,8 +238,9 @@ def main():
         if opq:
             ops_per_launch = opq * queries / (args.steps * launches_per_step * world)
             achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12
-            # the PMC passes ran this same command at N = 1 (config defaults: C5's subset)
-            ev = pmc_evidence(cfg.name) if (world == 1 and args.subset < 0 and not args.spp) else None
+            # the PMC passes ran this same command at N = 1 (config defaults: C5's subset, fast order)
+            same = world == 1 and args.subset < 0 and not args.spp and args.order == "fast"
+            ev = pmc_evidence(cfg.name) if same else None
             out["roofline"] = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS,
                                "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
                                "traffic": round(ev["hbm_bytes_per_launch"]) if ev else None,
