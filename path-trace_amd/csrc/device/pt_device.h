@@ -1516,18 +1516,129 @@ __device__ __forceinline__ V3 mirrorball_map(V3 v) /* transform_texture.h:46-59 
     float xt = v.x / d, yt = v.y / d;
     return mk((float)((double)xt * 0.5 + 0.5), (float)((double)yt * 0.5 + 0.5), 0);
 }
+/* The reference's std::atan2(float, float) and std::asin(float) are glibc's
+ * atan2f / asinf (oracle.cpp SphericalTex), which are not correctly rounded
+ * (16 % / 7 % of random operands differ from the rounded double result,
+ * profiles/round3/glibc_atan2f_asinf_vs_double.txt).  Restated here: the
+ * fdlibm float algorithms glibc 2.35 ships (flt-32 s_atanf / e_atan2f, and
+ * e_asinf with its p0..p4 minimax), plain f32 arithmetic without contraction;
+ * checked against glibc on the CPU (tools/libm: atan2f on 2e7 random
+ * operands, asinf on every float in [-1, 1], no difference). */
+__device__ __forceinline__ float libm_atanf(float x)
+{
+    constexpr float hi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
+    constexpr float lo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
+    const int hx = __float_as_int(x), ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x4c000000) {
+        if (ix > 0x7f800000)
+            return x + x;
+        return hx > 0 ? hi[3] + lo[3] : -hi[3] - lo[3];
+    }
+    if (ix < 0x3ee00000) {
+        if (ix < 0x31000000)
+            return x;
+        id = -1;
+    } else {
+        x = __builtin_fabsf(x);
+        if (ix < 0x3f980000) {
+            if (ix < 0x3f300000)
+                id = 0, x = (2.0f * x - 1.0f) / (2.0f + x);
+            else
+                id = 1, x = (x - 1.0f) / (x + 1.0f);
+        } else {
+            if (ix < 0x401c0000)
+                id = 2, x = (x - 1.5f) / (1.0f + 1.5f * x);
+            else
+                id = 3, x = -1.0f / x;
+        }
+    }
+    const float z = x * x, w = z * z;
+    const float s1 = z * (3.3333334327e-01f + w * (1.4285714924e-01f + w * (9.0908870101e-02f +
+                     w * (6.6610731184e-02f + w * (4.9768779427e-02f + w * 1.6285819933e-02f)))));
+    const float s2 = w * (-2.0000000298e-01f + w * (-1.1111110449e-01f + w * (-7.6918758452e-02f +
+                     w * (-5.8335702866e-02f + w * -3.6531571299e-02f))));
+    if (id < 0)
+        return x - x * (s1 + s2);
+    const float r = (id == 0 ? hi[0] : id == 1 ? hi[1] : id == 2 ? hi[2] : hi[3]) -
+                    ((x * (s1 + s2) - (id == 0 ? lo[0] : id == 1 ? lo[1] : id == 2 ? lo[2] : lo[3])) - x);
+    return hx < 0 ? -r : r;
+}
+__device__ __forceinline__ float libm_atan2f(float y, float x)
+{
+    constexpr float PI_O_2 = 1.5707963705e+00f, PI_F = 3.1415927410e+00f, PI_LO = -8.7422776573e-08f;
+    const int hx = __float_as_int(x), ix = hx & 0x7fffffff, hy = __float_as_int(y), iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000)
+        return x + y;
+    if (hx == 0x3f800000)
+        return libm_atanf(y);
+    int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if (iy == 0)
+        return m == 0 || m == 1 ? y : m == 2 ? PI_F : -PI_F;
+    if (ix == 0)
+        return hy < 0 ? -PI_O_2 : PI_O_2;
+    if (ix == 0x7f800000) {
+        const float PI_O_4 = 7.8539818525e-01f;
+        if (iy == 0x7f800000)
+            return m == 0 ? PI_O_4 : m == 1 ? -PI_O_4 : m == 2 ? 3.0f * PI_O_4 : -3.0f * PI_O_4;
+        return m == 0 ? 0.0f : m == 1 ? -0.0f : m == 2 ? PI_F : -PI_F;
+    }
+    if (iy == 0x7f800000)
+        return hy < 0 ? -PI_O_2 : PI_O_2;
+    const int k = (iy - ix) >> 23;
+    float z;
+    if (k > 26)
+        z = PI_O_2 + 0.5f * PI_LO, m &= 1;
+    else if (k < -26 && hx < 0)
+        z = 0.0f;
+    else
+        z = libm_atanf(__builtin_fabsf(y / x));
+    return m == 0 ? z : m == 1 ? -z : m == 2 ? PI_F - (z - PI_LO) : (z - PI_LO) - PI_F;
+}
+__device__ __forceinline__ float libm_asinf(float x)
+{
+    constexpr float PIO2_HI = 1.57079637050628662109375f, PIO2_LO = -4.37113900018624283e-8f,
+                    PIO4_HI = 0.785398185253143310546875f;
+    const int hx = __float_as_int(x), ix = hx & 0x7fffffff;
+    auto poly = [](float t) {
+        return t * (1.666675248e-1f + t * (7.495297643e-2f + t * (4.547037598e-2f + t * (2.417951451e-2f +
+               t * 4.216630880e-2f))));
+    };
+    if (ix == 0x3f800000)
+        return x * PIO2_HI + x * PIO2_LO;
+    if (ix > 0x3f800000)
+        return (x - x) / (x - x);
+    if (ix < 0x3f000000) {
+        if (ix < 0x32000000)
+            return x;
+        const float w = poly(x * x);
+        return x + x * w;
+    }
+    float t = (1.0f - __builtin_fabsf(x)) * 0.5f;
+    float p = poly(t);
+    const float s = __builtin_sqrtf(t);
+    if (ix >= 0x3F79999A) {
+        t = PIO2_HI - (2.0f * (s + s * p) - PIO2_LO);
+    } else {
+        const float w = __int_as_float(__float_as_int(s) & 0xfffff000);
+        const float c = (t - w * w) / (s + w);
+        p = 2.0f * s * p - (PIO2_LO - 2.0f * c);
+        t = PIO4_HI - (p - (PIO4_HI - 2.0f * w));
+    }
+    return hx > 0 ? t : -t;
+}
 __device__ __forceinline__ V3 spherical_map(V3 v) /* transform_texture.h:73-85 */
 {
     const double PI = 3.14159265358979323846;
     if (is_zero(v))
         return mk(0, 0, 0);
     v = normalize(v);
-    float theta = (float)atan2((double)v.y, (double)v.x);
+    float theta = libm_atan2f(v.y, v.x);
     if ((double)theta < -PI)
         theta = (float)((double)theta + 2 * PI);
     if ((double)theta > PI)
         theta = (float)((double)theta - 2 * PI);
-    float phi = (float)asin((double)v.z);
+    float phi = libm_asinf(v.z);
     return mk((float)((double)theta * 0.5 / PI + 0.5), (float)((double)phi / (PI / 2) * 0.5 + 0.5), 0);
 }
 template <class T>
