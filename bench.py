@@ -78,7 +78,11 @@ def parse():
                     help="0 = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS "
                          "when set (the GPU box exports its per-GPU CPU share there)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dump-frame", default="", help="rank 0: save the reduced frame (H x W x 3 f32 .npy)")
     ap.add_argument("--order", default="fast")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N>1: RCCL over xGMI (nccl), or gloo with the frame reduced through host memory -- "
+                         "rehearses the N>1 code path with several ranks on one GPU")
     ap.add_argument("--split", choices=["samples", "tiles"], default="samples",
                     help="N>1: each rank renders every pixel for its share of the samples (balanced to noise), "
                          "or the hashed 16x16 tiles it owns (bit-identical to 1 GPU, measured 1.19 max/mean "
@@ -154,13 +158,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = world > 1 and args.backend == "gloo"
+    if gloo:  # rehearsal: ranks may share a GPU
+        local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         dist = None
-        torch.cuda.set_device(local)
 
     cfg = scenes.CONFIGS[args.config]
     spp = args.spp or cfg.spp
@@ -183,33 +192,48 @@ def main():
     share.prepare()
     torch.cuda.synchronize()
 
-    def step():
-        fb.zero_()
-        st = share.render(fb.data_ptr(), stream.cuda_stream)
-        if dist is not None:
+    def reduce_frame():
+        if gloo:  # through host memory
+            h = fb.cpu()
+            dist.reduce(h, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                fb.copy_(h)
+        else:
             dist.reduce(fb, dst=0, op=dist.ReduceOp.SUM)
+
+    def step():
+        # the render is queued without a host wait (its HIP-event timings are
+        # collected after the timed region): the reduce follows it on the stream
+        fb.zero_()
+        share.render_async(fb.data_ptr(), stream.cuda_stream)
+        if dist is not None:
+            reduce_frame()
             share.finish(fb)  # rank 0, sample split: the ranks' sums over spp
-        return st
 
     for _ in range(args.warmup):
         step()
+    torch.cuda.synchronize()
+    share.collect()  # drop the warm-up timings
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats = [step() for _ in range(args.steps)]
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = sum(s["kernel_ms"] for s in stats) / max(1, sum(s["launches"] for s in stats))
-    launches_per_step = stats[0]["launches"]
-    queries = sum(s["queries"] for s in stats)
+    st = share.collect()
+    kernel_ms = st["kernel_ms"] / max(1, st["launches"])
+    launches_per_step = st["launches"] // max(1, args.steps)
+    queries = st["queries"]
     if dist is not None:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        dev = "cpu" if gloo else "cuda"
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
-        q = torch.tensor([queries], dtype=torch.float64, device="cuda")
+        q = torch.tensor([queries], dtype=torch.float64, device=dev)
         dist.all_reduce(q, op=dist.ReduceOp.SUM)
         queries = int(q[0])
 
@@ -218,6 +242,8 @@ def main():
         samples = npix_total * spp * args.steps
         value = samples / elapsed / 1e6
         frame = fb.view(H, W, 3).cpu().numpy()
+        if args.dump_frame:
+            np.save(args.dump_frame, frame)
         out = {
             "metric": "Msamples/sec at 1920x1080x1024spp; per-channel RMSE vs CPU ref",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
@@ -229,8 +255,10 @@ def main():
                        "order": args.order,
                        "sharding": (("one GPU renders every pixel" if not subset else
                                      "one GPU renders %d hashed pixels of the frame" % subset) if world == 1 else
-                                    "every pixel, spp split over ranks, per-pixel sums + RCCL reduce" if by_samples
-                                    else "16x16 tiles hashed over ranks + RCCL reduce")},
+                                    ("every pixel, spp split over ranks, per-pixel sums" if by_samples
+                                     else "16x16 tiles hashed over ranks") +
+                                    (" + gloo reduce through host memory (rehearsal: %d ranks on %d GPU(s))" %
+                                     (world, torch.cuda.device_count()) if gloo else " + RCCL reduce"))},
             "samples_per_step": npix_total * spp,
             "queries_per_sample": round(queries / samples, 2),
         }

@@ -684,6 +684,22 @@ public:
     {
         q_->id = o->flatten(q_->f);
     }
+    /* tracePixel's device side: this iterator's object as a render root
+     * (set once), npixels pixel indices of a grid grid_width wide */
+    void renderPixels(const int32_t *pixels, int64_t npixels, int W, int H, int grid_width, int spp, int depth,
+                      float sw, float sh, float dist, uint64_t seed, int order, float *rgb) const
+    {
+        if (!root_set_) {
+            ptCheck(pt_set_root(q_->s, q_->id));
+            root_set_ = true;
+        }
+        pt_render_params p = {};
+        p.width = W, p.height = H, p.spp = spp, p.depth = depth;
+        p.screen_w = sw, p.screen_h = sh, p.screen_dist = dist;
+        p.seed = seed, p.order = order, p.grid_width = grid_width;
+        p.pixels = pixels, p.npixels = npixels;
+        ptCheck(pt_render(q_->s, &p, rgb, nullptr));
+    }
     const Span &operator*() const override { return spans_.at(k_); }
     const Span *operator->() const override { return &spans_.at(k_); }
     bool isAtEnd() const override { return k_ >= spans_.size(); }
@@ -716,9 +732,108 @@ private:
     std::unique_ptr<DeviceQueryScene> q_;
     std::vector<Span> spans_;
     size_t k_ = 0;
+    mutable bool root_set_ = false;
 };
 
 inline SpanIterator *Object::makeSpanIterator() const { return new DeviceSpanIterator(this); }
+
+/* -------------------------------------------------------------- tracePixel -- */
+const int DefaultRayDepth = 16;          /* include/path-trace.h:57  */
+const int DefaultSampleCount = 200;      /* include/path-trace.h:167 */
+const float DefaultScreenWidth = 4.0 / 3.0, DefaultScreenHeight = 1.0, DefaultScreenDistance = 2.0; /* :168-170 */
+
+/* The engine argument of tracePixel (include/path-trace.h:187-201 takes the
+ * caller's `T &randomEngine` and draws every sample of every pixel from it in
+ * sequence).  The device gives each (pixel, sample) an engine of its own,
+ * keyed from a run seed (include/pt/pt_engine.h), so the samples of many
+ * pixels run side by side: calls with the same FrameEngine return, pixel by
+ * pixel, the bits Renderer::render returns for the frame with that seed and
+ * order -- in any call order, from any thread. */
+struct FrameEngine
+{
+    uint64_t seed;
+    int order;
+    explicit FrameEngine(uint64_t seed = 0x5EED, int order = PT_ORDER_FAST) : seed(seed), order(order) {}
+};
+
+/* the global engine of the non-template overload (the reference's defaultRandomEngine, path-trace.h:56) */
+inline FrameEngine &defaultFrameEngine()
+{
+    static FrameEngine e;
+    return e;
+}
+
+/* tracePixel(SpanIterator &, int px, int py, ...) of include/path-trace.h:187-201
+ * over a batch: colors[k] = the mean radiance of pixel (px[k], py[k]).  The span
+ * iterator must be a built-in object's (Object::makeSpanIterator): its object is
+ * the scene the device renders.  One device launch for the whole batch.
+ * Pixels past the right edge (the adaptive caller's block corners at x ==
+ * screenXResolution, src/test.cpp:466-499) are keyed on a grid one wider. */
+inline void tracePixels(SpanIterator &spanIterator, const int32_t *px, const int32_t *py, size_t n, Color *colors,
+                        int screenXResolution, int screenYResolution, int sampleCount, int rayDepth, float screenWidth,
+                        float screenHeight, float screenDistance, const FrameEngine &engine)
+{
+    DeviceSpanIterator *it = dynamic_cast<DeviceSpanIterator *>(&spanIterator);
+    if (!it)
+        throw DeviceError(PT_ERR_ARG, "tracePixel: needs the span iterator of a built-in object "
+                                      "(Object::makeSpanIterator)");
+    if (n == 0)
+        return;
+    int gw = screenXResolution;
+    for (size_t k = 0; k < n; k++) {
+        if (px[k] < 0 || py[k] < 0)
+            throw std::invalid_argument("tracePixel: negative pixel coordinate");
+        if (px[k] >= gw)
+            gw = px[k] + 1;
+    }
+    std::vector<int32_t> pix(n);
+    for (size_t k = 0; k < n; k++) {
+        const int64_t i = (int64_t)py[k] * gw + px[k];
+        if (i > INT32_MAX)
+            throw std::invalid_argument("tracePixel: pixel index out of range");
+        pix[k] = (int32_t)i;
+    }
+    static_assert(sizeof(Color) == 3 * sizeof(float), "Color must be 3 packed floats");
+    it->renderPixels(pix.data(), (int64_t)n, screenXResolution, screenYResolution, gw, sampleCount, rayDepth,
+                     screenWidth, screenHeight, screenDistance, engine.seed, engine.order,
+                     reinterpret_cast<float *>(colors));
+}
+
+inline Color tracePixel(SpanIterator &spanIterator, int px, int py, int screenXResolution, int screenYResolution,
+                        int sampleCount, int rayDepth, float screenWidth, float screenHeight, float screenDistance,
+                        FrameEngine &randomEngine)
+{
+    const int32_t x = px, y = py;
+    Color c;
+    tracePixels(spanIterator, &x, &y, 1, &c, screenXResolution, screenYResolution, sampleCount, rayDepth,
+                screenWidth, screenHeight, screenDistance, randomEngine);
+    return c;
+}
+
+/* Any other engine type T (unsigned operator()(), as include/vector3d.h:14-34
+ * requires of it -- e.g. the reference's DefaultRandomEngine): two of its
+ * draws make the run seed of this call, so successive calls see fresh
+ * streams as with the reference's shared engine. */
+template <typename T>
+inline Color tracePixel(SpanIterator &spanIterator, int px, int py, int screenXResolution, int screenYResolution,
+                        int sampleCount, int rayDepth, float screenWidth, float screenHeight, float screenDistance,
+                        T &randomEngine)
+{
+    const uint64_t hi = (uint32_t)randomEngine(), lo = (uint32_t)randomEngine();
+    FrameEngine e((hi << 32) | lo);
+    return tracePixel(spanIterator, px, py, screenXResolution, screenYResolution, sampleCount, rayDepth,
+                      screenWidth, screenHeight, screenDistance, e);
+}
+
+/* the non-template overload (include/path-trace.h:203-206): the global engine */
+inline Color tracePixel(SpanIterator &spanIterator, int px, int py, int screenXResolution, int screenYResolution,
+                        int sampleCount = DefaultSampleCount, int rayDepth = DefaultRayDepth,
+                        float screenWidth = DefaultScreenWidth, float screenHeight = DefaultScreenHeight,
+                        float screenDistance = DefaultScreenDistance)
+{
+    return tracePixel(spanIterator, px, py, screenXResolution, screenYResolution, sampleCount, rayDepth, screenWidth,
+                      screenHeight, screenDistance, defaultFrameEngine());
+}
 
 class TransformedObject : public Object /* object.h:26-98 */
 {

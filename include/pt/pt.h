@@ -114,6 +114,7 @@ void pt_matrix_concat(const float a[12], const float b[12], float out[12]);
                                 lane sums, added as their pairwise tree; samples in
                                 32-sample pairwise blocks (oracle.cpp ORDER_FAST)     */
 #define PT_ORDER_REFERENCE 1 /* bit-for-bit the reference's sequential child order          */
+#define PT_ORDER_GROUP64 PT_ORDER_FAST /* deprecated name of PT_ORDER_FAST (rounds 1-2)      */
 
 typedef struct pt_render_params {
     int width, height;             /* screenXResolution, screenYResolution                      */
@@ -168,6 +169,18 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
  * given hipStream_t (NULL = default stream) and returns once the work is
  * enqueued... or completed when stats != NULL (stats need the timings). */
 int pt_render_device(pt_scene *s, const pt_render_params *p, float *fb, void *stream, pt_render_stats *stats);
+
+/* pt_render_device that stays asynchronous and still keeps its timings: HIP
+ * events around each launch and the device counters accumulate on the scene's
+ * device until pt_render_collect, so a caller can queue the render, a
+ * collective on the same stream and more renders without a host round trip
+ * (bench.py's multi-GPU step: render, then the RCCL reduce of the frame). */
+int pt_render_device_timed(pt_scene *s, const pt_render_params *p, float *fb, void *stream);
+
+/* Waits for the timed renders queued on `device` since the last collect and
+ * returns their summed statistics (kernel_ms, launches, samples, counters);
+ * all zero when none are pending. */
+int pt_render_collect(pt_scene *s, int device, pt_render_stats *stats);
 
 /* The reference demo's image-formation policy, RenderBlock::renderSquare
  * (src/test.cpp:423-507): per block of block_size x block_size pixels, trace
@@ -267,6 +280,13 @@ int pt_query_compile(pt_scene *s, pt_id obj, pt_id tex);
  * normalize against the compiler's correctly rounded ones on n hashed inputs.
  * mismatches[0..2] receive the sqrt, div and normalize mismatch counts. */
 int pt_selftest_math(int device, uint64_t n, uint64_t seed, uint64_t *mismatches);
+
+/* Device self-test of the restated glibc float libm the texture maps use
+ * (SphericalCoordinatesSkymapTexture's atan2f / asinf, transform_texture.h:
+ * 73-85; LogTexture's logf, filter_texture.h:62-67): for n operand pairs
+ * ops[2i] = y, ops[2i+1] = x, out[3i..3i+2] = atan2f(y, x), asinf(y), logf(x)
+ * as the device computes them, for comparison with the host's libm. */
+int pt_selftest_libm(int device, const float *ops, int64_t n, float *out);
 
 /* ------------------------------------------------------------- output --- */
 /* MutableImage::writeHDR (reference src/image.cpp:398-481), rgb = w*h*3 floats. */

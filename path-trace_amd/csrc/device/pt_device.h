@@ -1487,11 +1487,68 @@ struct TMul /* MultiplyTexture */
     }
     __device__ static __forceinline__ float value(V3 p, const Env &e) { return mean3(color(p, e)); }
 };
-__device__ __forceinline__ float log_filter(float v) /* filter_texture.h:66-71 */
+/* The reference's std::log(float) is glibc's logf, which is not correctly
+ * rounded: (float)log((double)x) differs from it on 416 909 of the 2^31 - 2^23
+ * finite positive floats.  Restated: glibc 2.35's sysdeps/ieee754/flt-32/
+ * e_logf.c (Szabolcs Nagy, ARM optimized-routines; MIT/BSD-style licence, see
+ * tools/libm/logf_restated.c): a 16-entry table of (1/c, log c), log1p of
+ * z/c - 1 by a degree-3 polynomial, all in double.  Checked on the CPU against
+ * glibc on every non-negative float, with and without FMA contraction of the
+ * double arithmetic (glibc ships FMA variants): no difference
+ * (tools/libm/logf_restated.c). */
+__device__ __forceinline__ double logf_tab(int i, int hi)
+{
+    /* (invc, logc) pairs, __logf_data.tab */
+    constexpr double T[32] = {
+        0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2, 0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2,
+        0x1.49539f0f010bp+0,  -0x1.01eae7f513a67p-2, 0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3,
+        0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3, 0x1.25e227b0b8eap+0,  -0x1.1aa2bc79c81p-3,
+        0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4, 0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4,
+        0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5, 0x1p+0,               0x0p+0,
+        0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5,  0x1.ca4b31f026aap-1,  0x1.c5e53aa362eb4p-4,
+        0x1.b2036576afce6p-1, 0x1.526e57720db08p-3,  0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3,
+        0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2,  0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2};
+    double r = T[hi];
+#pragma unroll
+    for (int k = 1; k < 16; k++) /* selects, not a private array indexed per lane */
+        r = i == k ? T[2 * k + hi] : r;
+    return r;
+}
+__device__ __forceinline__ float libm_logf(float x)
+{
+    constexpr double LN2 = 0x1.62e42fefa39efp-1, A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2,
+                     A2 = -0x1.ffffef20a4123p-2;
+    u32 ix = __float_as_uint(x);
+    if (ix == 0x3f800000u)
+        return 0.0f;
+    if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
+        if (ix * 2u == 0u)
+            return -__builtin_inff();
+        if (ix == 0x7f800000u)
+            return x;
+        if ((ix & 0x80000000u) || ix * 2u >= 0xff000000u)
+            return __builtin_nanf("");
+        ix = __float_as_uint(x * 0x1p23f); /* subnormal: normalise */
+        ix -= 23u << 23;
+    }
+    const u32 tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) % 16u), k = (int)tmp >> 23;
+    const u32 iz = ix - (tmp & (0x1ffu << 23));
+    const double invc = logf_tab(i, 0), logc = logf_tab(i, 1);
+    const double z = (double)__uint_as_float(iz);
+    const double r = z * invc - 1.0;
+    const double y0 = logc + (double)k * LN2;
+    const double r2 = r * r;
+    double y = A1 * r + A2;
+    y = A0 * r2 + y;
+    y = y * r2 + (y0 + r);
+    return (float)y;
+}
+__device__ __forceinline__ float log_filter(float v) /* filter_texture.h:62-67 */
 {
     if ((double)v <= 1e-30)
         return 0.0f;
-    return 0.5f + (float)log((double)v) / 0.693147182f / 256.0f;
+    return 0.5f + libm_logf(v) / 0.693147182f / 256.0f;
 }
 template <class T>
 struct TLog /* LogTexture */
@@ -1523,7 +1580,16 @@ __device__ __forceinline__ V3 mirrorball_map(V3 v) /* transform_texture.h:46-59 
  * fdlibm float algorithms glibc 2.35 ships (flt-32 s_atanf / e_atan2f, and
  * e_asinf with its p0..p4 minimax), plain f32 arithmetic without contraction;
  * checked against glibc on the CPU (tools/libm: atan2f on 2e7 random
- * operands, asinf on every float in [-1, 1], no difference). */
+ * operands plus 2.4e6 edge operands -- exponent gaps of -140..127, signed
+ * zeros, infinities, NaN --, asinf on every float in [-1, 1]: no
+ * difference), and on the GPU against the host's glibc by pt_selftest_libm.
+ *
+ * fdlibm notice (the algorithms and constants below are Sun's):
+ *   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ *   Developed at SunPro, a Sun Microsystems, Inc. business.
+ *   Permission to use, copy, modify, and distribute this software is freely
+ *   granted, provided that this notice is preserved.
+ *   (Conversion to float by Ian Lance Taylor, Cygnus Support.) */
 __device__ __forceinline__ float libm_atanf(float x)
 {
     constexpr float hi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
@@ -1587,9 +1653,9 @@ __device__ __forceinline__ float libm_atan2f(float y, float x)
         return hy < 0 ? -PI_O_2 : PI_O_2;
     const int k = (iy - ix) >> 23;
     float z;
-    if (k > 26)
-        z = PI_O_2 + 0.5f * PI_LO, m &= 1;
-    else if (k < -26 && hx < 0)
+    if (k > 60) /* glibc's flt-32 thresholds (FreeBSD's 26 with m &= 1 differs for gaps of 27..60) */
+        z = PI_O_2 + 0.5f * PI_LO;
+    else if (k < -60 && hx < 0)
         z = 0.0f;
     else
         z = libm_atanf(__builtin_fabsf(y / x));
@@ -1689,6 +1755,27 @@ __device__ __forceinline__ void cadd(u64 &c, u32 v)
     if ((threadIdx.x & 63) == 0)
         __hip_atomic_fetch_add(&c, (u64)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
+
+/* LCG jumps in LDS, shared by the workgroup's waves: j3[l] = (A, G * inc) of
+ * 3l draws (attempt l of a round, lane l in attempt-major rounds; k < 8: the
+ * offset of a lane-major round's k-th attempt), j24[l] = the same for 24l
+ * draws (lane l's first attempt, 8l, in a lane-major round).  Read through
+ * volatile loads where a round needs them: hoisted out of the burst loop
+ * they would be held in registers and spilled to scratch. */
+struct JumpLds
+{
+    const u64 (*j3)[2];
+    const u64 (*j24)[2];
+};
+__device__ __forceinline__ void jread(const u64 (*t)[2], int i, u64 &A, u64 &G)
+{
+    const volatile u64 *p = t[i];
+    A = p[0];
+    G = p[1];
+}
+#ifndef PT_LANE_MAJOR
+#define PT_LANE_MAJOR 1 /* deferred rounds: lane l evaluates attempts 8l..8l+7 (one chained stream) */
+#endif
 
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
@@ -1812,10 +1899,27 @@ struct Attempt2
     bool acc[2];
 };
 template <bool KR0>
+__device__ __forceinline__ Attempt2 attempt2_draws(W2 a1, W2 a2, W2 a3, W2 b1, W2 b2, W2 b3, V3 n, V3 kR);
+template <bool KR0>
 __device__ __forceinline__ Attempt2 attempt2(u64 s0a, u64 s0b, V3 n, V3 kR)
 {
     const W2 a1 = lcg_step({(u32)s0a, (u32)(s0a >> 32)}), a2 = lcg_step(a1), a3 = lcg_step(a2);
     const W2 b1 = lcg_step({(u32)s0b, (u32)(s0b >> 32)}), b2 = lcg_step(b1), b3 = lcg_step(b2);
+    return attempt2_draws<KR0>(a1, a2, a3, b1, b2, b3, n, kR);
+}
+/* Two CONSECUTIVE attempts of one lane's stream (lane-major rounds): the
+ * second starts where the first's three draws end; s advances past both. */
+template <bool KR0>
+__device__ __forceinline__ Attempt2 attempt2_chain(u64 &s, V3 n, V3 kR)
+{
+    const W2 a1 = lcg_step({(u32)s, (u32)(s >> 32)}), a2 = lcg_step(a1), a3 = lcg_step(a2);
+    const W2 b1 = lcg_step(a3), b2 = lcg_step(b1), b3 = lcg_step(b2);
+    s = ((u64)b3.hi << 32) | (u64)b3.lo;
+    return attempt2_draws<KR0>(a1, a2, a3, b1, b2, b3, n, kR);
+}
+template <bool KR0>
+__device__ __forceinline__ Attempt2 attempt2_draws(W2 a1, W2 a2, W2 a3, W2 b1, W2 b2, W2 b3, V3 n, V3 kR)
+{
     const f2 S = 0x1p-31f, M1 = -1.0f;
     /* u11: (float)o * 2^-31 - 1, the product exact (see u11) */
     f2 x = {(float)a1.hi, (float)b1.hi}, y = {(float)a2.hi, (float)b2.hi}, z = {(float)a3.hi, (float)b3.hi};
@@ -1927,7 +2031,7 @@ __device__ __forceinline__ int replay(u64 A, u64 F, u64 NL, int rem, int &fails,
  * the next child's ray into `child` when that child must recurse (it draws
  * random numbers, so it runs on the spine). */
 template <class S, bool STRICT, bool DEFERRED, bool KR0>
-__device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, const u64 *jl,
+__device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__restrict__ jump, const JumpLds &J,
                                        const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
     float4 *const ring = L.ring;
@@ -1946,8 +2050,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const bool child_leaf_depth = depth - 1 <= 0;
     /* lane l's state 3l draws into the round (attempt l): its jump (A, G)
      * is read from LDS where a round needs it, not held in registers */
-    const u64 jA = jl[0], jG = jl[1] * LCG_INC;
-    auto lane_state = [&]() { return jA * rng.st + jG; };
+    auto lane_state = [&]() {
+        u64 jA, jG;
+        jread(J.j3, lane, jA, jG);
+        return jA * rng.st + jG;
+    };
+    /* lane-major rounds (deferred bursts): lane l's first attempt is 8l */
+    constexpr bool LMAJ = DEFERRED && PT_LANE_MAJOR && PT_KATT_SHORT == PT_KATT;
     const u64 A64 = jump[128], g64inc = jump[129] * LCG_INC;   /* 64 attempts = 192 draws  */
     const u64 Afull = jump[128 * PT_KATT], gfullinc = jump[128 * PT_KATT + 1] * LCG_INC; /* a full round */
     int fails = 0, reason = -1;
@@ -2053,7 +2162,60 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 ta += __popcll(A);
                 tk += __popcll(kp);
             };
-            if (DEFERRED) {
+            int fails_lm = 0; /* lane-major: the consecutive failures after the round */
+            if constexpr (LMAJ) {
+                /* Lane-major round: lane l evaluates attempts 8l .. 8l+7, one
+                 * chained stream (no jump between its attempts), in packed
+                 * pairs.  Child order is attempt order j = 8l + k: the kept
+                 * attempts of lanes below come first, so the ring slots are
+                 * numbered once the round's kept masks are known, and a slot
+                 * parks the lane's round state and k (the first pass jumps 3k
+                 * draws).  tf = this lane's hemisphere failures after its
+                 * last accepted attempt. */
+                u64 jA, jG;
+                jread(J.j24, lane, jA, jG);
+                const u64 s_lane = jA * rng.st + jG;
+                u64 sk = s_lane;
+                int tf = 0;
+                u64 Aor = 0ull, K[PT_KATT];
+#pragma unroll
+                for (int k = 0; k < PT_KATT; k += 2) {
+                    const Attempt2 ap = attempt2_chain<KR0>(sk, n, kR);
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
+                        u64 D = 0ull;
+                        if (RAW)
+                            D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
+                        K[k + h] = ap.A[h] & ~D;
+                        ta += __popcll(ap.A[h]);
+                        tk += __popcll(K[k + h]);
+                        Aor |= ap.A[h];
+                        tf = mask_sel(ap.A[h], 0, tf + lane_bit(ap.F[h]));
+                    }
+                }
+                /* ring entries, numbered in child order */
+                int slot = nkeep;
+#pragma unroll
+                for (int k = 0; k < PT_KATT; k++)
+                    slot = mbcnt(K[k], slot);
+#pragma unroll
+                for (int k = 0; k < PT_KATT; k++) {
+                    if (in_mask(K[k] & __ballot(slot < slot_end)))
+                        ring[slot & (PT_RCAP - 1)] = make_float4(__uint_as_float((u32)s_lane),
+                                                                 __uint_as_float((u32)(s_lane >> 32)),
+                                                                 __int_as_float(k), 0.0f);
+                    slot += lane_bit(K[k]);
+                }
+                /* failures after the round's last accepted attempt (lane L,
+                 * then every lane above it); none accepted: all of them */
+                const u64 GE = Aor ? ~0ull << (63 - __builtin_clzll(Aor)) : ~0ull;
+                int sf = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++)
+                    sf += __popcll(__ballot((tf >> b) & 1) & GE) << b;
+                fails_lm = Aor ? sf : fails + sf;
+            } else if (DEFERRED) {
                 /* pairs of attempts in packed f32 */
                 u64 sk = lane_state();
 #pragma unroll
@@ -2105,9 +2267,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
              * attempts stay below 1000) -- so every half takes all its
              * accepted attempts, and the consecutive-failure count afterwards
              * is that of the last half, which has an accepted attempt. */
-            if (nlor == 0ull && ta < rem && tk <= free_slots && fails <= 999 - 64 * katt && Alast != 0ull) {
-                const int last = 63 - __builtin_clzll(Alast);
-                fails = (last == 63) ? 0 : __popcll(Flast >> (last + 1));
+            if (nlor == 0ull && ta < rem && tk <= free_slots && fails <= 999 - 64 * katt && (LMAJ || Alast != 0ull)) {
+                if (LMAJ) {
+                    fails = fails_lm;
+                } else {
+                    const int last = 63 - __builtin_clzll(Alast);
+                    fails = (last == 63) ? 0 : __popcll(Flast >> (last + 1));
+                }
                 m = 64 * katt;
                 np = ta;
                 nk = tk;
@@ -2330,6 +2496,11 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                          * left to this pass so that 64 useful lanes do them */
                         u64 st;
                         __builtin_memcpy(&st, &en, 8);
+                        if (LMAJ) { /* the lane's round state, then 3k draws to attempt k */
+                            u64 jA, jG;
+                            jread(J.j3, __float_as_int(en.z), jA, jG);
+                            st = jA * st + jG;
+                        }
                         const W2 s1 = lcg_step({(u32)st, (u32)(st >> 32)}), s2 = lcg_step(s1), s3 = lcg_step(s2);
                         V3 w = mk(u11(s1.hi), u11(s2.hi), u11(s3.hi));
                         if (!KR0)
@@ -2451,7 +2622,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
  * normalised direction / factor are computed per child at trace time (same
  * arithmetic, same bits) with every lane busy. */
 template <class S, bool STRICT>
-__device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, const u64 *jl,
+__device__ __forceinline__ int burst(const Env &e, Rng &rng, const u64 *__restrict__ jump, const JumpLds &jl,
                                      const WaveLds &L, Frame &f, Frame &child, Counters &cnt)
 {
     const float sNa = unif((unif(f.strength) / (float)uni(f.N)) * unif(f.add));
@@ -2993,7 +3164,7 @@ __device__ __forceinline__ bool lane_walk_sc(const Env &e, int depth0, V3 d0, co
 
 template <class S, int MAXD, bool STRICT>
 __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int pix, int s, Frame *F, const WaveLds &L,
-                                           const u64 *__restrict__ jump, const u64 *jl, Counters &cnt,
+                                           const u64 *__restrict__ jump, const JumpLds &jl, Counters &cnt,
                                            const CamHit &cam)
 {
     Rng rng;
@@ -3201,13 +3372,14 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     __shared__ unsigned char mbuf[PT_WPW][PT_SCAP];
     __shared__ Counters cbuf[PT_WPW];
     /* a chunk's lanes while the wave walks its samples one by one: (pixel,
-     * sample | hit << 30 | exit << 31, camera t, camera ref) and the results,
-     * in LDS rather than in registers that would stay live through every
-     * burst (the allocator spilled them to scratch) */
+     * sample | hit << 30 | exit << 31, camera t, camera ref), replaced by the
+     * sample's result (x, y, z) once it is traced; in LDS rather than in
+     * registers that would stay live through every burst (the allocator
+     * spilled them to scratch) */
     __shared__ uint4 lbuf[PT_WPW][64];
-    __shared__ float obuf[PT_WPW][64 * 3];
-    /* lane l's engine jump of 3l draws (A, G): read by each generation round */
+    /* engine jumps of 3l and 24l draws (A, G * inc): JumpLds */
     __shared__ u64 jbuf[64][2];
+    __shared__ u64 jbuf24[64][2];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const u64 t_start = __builtin_amdgcn_s_memrealtime(); /* 100 MHz: wave lifetimes, stats[26..29] */
     const Env e = {P, imgs};
@@ -3222,14 +3394,18 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                 ((u32 *)p)[k] = 0xFFFFFFFFu;
         };
         poison(stk, sizeof stk), poison(xbuf, sizeof xbuf), poison(rbuf, sizeof rbuf), poison(sbuf, sizeof sbuf);
-        poison(mbuf, sizeof mbuf), poison(cbuf, sizeof cbuf), poison(lbuf, sizeof lbuf), poison(obuf, sizeof obuf);
-        poison(jbuf, sizeof jbuf);
+        poison(mbuf, sizeof mbuf), poison(cbuf, sizeof cbuf), poison(lbuf, sizeof lbuf);
+        poison(jbuf, sizeof jbuf), poison(jbuf24, sizeof jbuf24);
         __syncthreads();
     }
 #endif
-    if (wave == 0)
-        jbuf[lane][0] = jump[2 * lane], jbuf[lane][1] = jump[2 * lane + 1];
+    for (int i = threadIdx.x; i < 128; i += 64 * PT_WPW) {
+        const int l = i & 63, m = i < 64 ? l : 8 * l; /* m attempts = 3m draws */
+        u64 *t = i < 64 ? jbuf[l] : jbuf24[l];
+        t[0] = jump[2 * m], t[1] = jump[2 * m + 1] * LCG_INC;
+    }
     __syncthreads();
+    const JumpLds jl = {jbuf, jbuf24};
     Counters &cnt = cbuf[wave];
     cnt.queries = cnt.leaf = cnt.attempts = cnt.rounds = cnt.shaded = cnt.nonleaf = cnt.slow = cnt.dark = 0;
     cnt.mid = 0;
@@ -3313,25 +3489,26 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         }
         /* park the lanes' state in LDS for the walks below */
         uint4 *const lb = lbuf[wave];
-        float *const ob = obuf[wave];
-        lb[lane] = make_uint4((u32)lpix, (u32)ls | ((u32)ch.hit << 30) | ((u32)ch.ex << 31), __float_as_uint(ch.t),
-                              ch.ref);
-        ob[3 * lane] = lres.x, ob[3 * lane + 1] = lres.y, ob[3 * lane + 2] = lres.z; /* valid where ldone */
+        const bool lwalk = lvalid && !ldone;
+        lb[lane] = lwalk ? make_uint4((u32)lpix, (u32)ls | ((u32)ch.hit << 30) | ((u32)ch.ex << 31),
+                                      __float_as_uint(ch.t), ch.ref)
+                         : make_uint4(__float_as_uint(lres.x), __float_as_uint(lres.y), __float_as_uint(lres.z), 0u);
         /* the other items, one after another by the whole wave; only this mask
          * stays live across the walks */
-        for (u64 todo = __ballot(lvalid) & ~__ballot(ldone); todo; todo &= todo - 1) {
+        for (u64 todo = __ballot(lwalk); todo; todo &= todo - 1) {
             const int j = uni(__builtin_ctzll(todo));
             PT_T0(tt);
             const uint4 q = lb[j];
             const int qy = uni((int)q.y);
             const CamHit cam = {(qy >> 30) & 1, unif(__uint_as_float(q.z)), (u32)uni((int)q.w), (int)((u32)qy >> 31)};
-            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni((int)q.x), qy & 0x3FFFFFFF, stk[wave], L, jump,
-                                                 jbuf[lane], cnt, cam);
+            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni((int)q.x), qy & 0x3FFFFFFF, stk[wave], L, jump, jl, cnt,
+                                                 cam);
             PT_ACC(cnt, 6, tt);
             if (lane == j)
-                ob[3 * j] = c.x, ob[3 * j + 1] = c.y, ob[3 * j + 2] = c.z;
+                lb[j] = make_uint4(__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), 0u);
         }
-        const V3 mine = mk(ob[3 * lane], ob[3 * lane + 1], ob[3 * lane + 2]);
+        const uint4 mr = lb[lane];
+        const V3 mine = mk(__uint_as_float(mr.x), __uint_as_float(mr.y), __uint_as_float(mr.z));
 #if !PT_DEQUEUE_PREFETCH
         next = dequeue();
 #endif
@@ -3403,8 +3580,8 @@ template <class S, int MAXD>
 __device__ constexpr int min_workgroups()
 {
     constexpr int lds = PT_WPW * ((MAXD + 1) * (int)sizeof(Frame) + 16 * PT_RCAP + 2 * PT_SCAP +
-                                  (int)sizeof(Counters) + (int)sizeof(typename S::Root::Ctx) + 64 * (16 + 12)) +
-                        64 * 16;
+                                  (int)sizeof(Counters) + (int)sizeof(typename S::Root::Ctx) + 64 * 16) +
+                        2 * 64 * 16;
     constexpr int alloc = (lds + 1279) / 1280 * 1280; /* gfx950 LDS allocation unit (measured) */
     constexpr int n = 160 * 1024 / alloc;
     return n < 1 ? 1 : n > 5 ? 5 : n;
@@ -3623,5 +3800,18 @@ extern "C" __global__ void pt_selftest_math(u64 n, u64 seed, unsigned long long 
         atomicAdd(&bad[1], bd);
     if (bn)
         atomicAdd(&bad[2], bn);
+}
+/* The restated glibc float libm (libm_atan2f, libm_asinf, libm_logf) on
+ * caller operands: out[3i..3i+2] = atan2f(ops[2i], ops[2i+1]),
+ * asinf(ops[2i]), logf(ops[2i+1]); the caller compares with its host's glibc
+ * (tests/test_libm.py). */
+extern "C" __global__ void pt_selftest_libm(const float *ops, u64 n, float *out)
+{
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const float y = ops[2 * i], x = ops[2 * i + 1];
+        out[3 * i] = ptd::libm_atan2f(y, x);
+        out[3 * i + 1] = ptd::libm_asinf(y);
+        out[3 * i + 2] = ptd::libm_logf(x);
+    }
 }
 #endif

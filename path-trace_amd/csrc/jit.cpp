@@ -87,6 +87,11 @@ const char *kOptions[] = {
      * C2 and C5 unchanged within noise) */
     "-mllvm",
     "-split-spill-mode=size",
+    /* LDS is sized by hand for the workgroups-per-CU target (min_workgroups);
+     * private arrays the promoter would move into spare LDS can push a
+     * workgroup past the CU's 160 KB / 1280-B granule budget */
+    "-mllvm",
+    "-disable-promote-alloca-to-lds",
 };
 
 /* experiment hook: extra compiler options, e.g. PT_JIT_OPTIONS="-fno-slp-vectorize".

@@ -97,6 +97,15 @@ struct DevBuf
     }
 };
 
+/* The HIP events and sample count of one render whose timings are not read yet */
+struct PendingRender
+{
+    std::vector<hipEvent_t> evs;
+    std::vector<std::pair<int, int>> spans, rspans; /* (start, end) event of each render / reduce launch */
+    uint64_t samples = 0;
+    int n_spheres = 0, n_planes = 0;
+};
+
 struct DeviceState
 {
     int device = 0;
@@ -114,10 +123,13 @@ struct DeviceState
     DevBuf<float> stage, accum, fb;
     DevBuf<int> pixels;
     DevBuf<uint64_t> stats;
+    std::vector<PendingRender> pending; /* deferred timings (pt_render_device_timed) */
     ~DeviceState()
     {
         int prev = 0;
         if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(device) == hipSuccess) {
+            for (auto &pr : pending)
+                for (auto e : pr.evs) (void)hipEventDestroy(e);
             P.release(), imgs.release(), jump.release(), stage.release(), accum.release(), fb.release();
             pixels.release(), stats.release();
             for (auto &b : img_data) b.release();
@@ -604,11 +616,83 @@ DeviceState &prepare(SceneImpl &s, const pt_render_params *p, Generated &g)
     return ds;
 }
 
-void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream_t stream, pt_render_stats *st)
+/* How a render reports its timings: not at all, synchronously (the call waits
+ * for the kernels and fills pt_render_stats), or deferred (HIP events and the
+ * device counters accumulate in the device state until pt_render_collect, so
+ * the render stays asynchronous on the caller's stream: bench.py's reduce
+ * follows it without a host round trip). */
+enum class Timing
+{
+    None,
+    Sync,
+    Deferred
+};
+
+/* Reads the recorded launches and the device counters of ds into st (after the
+ * last recorded event completes) and forgets them. */
+void collect_timings(DeviceState &ds, pt_render_stats *st)
+{
+    memset(st, 0, sizeof(*st));
+    if (ds.pending.empty())
+        return;
+    HIPCHECK(hipEventSynchronize(ds.pending.back().evs.back()));
+    for (auto &pr : ds.pending) {
+        for (auto &sp : pr.spans) {
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, pr.evs[sp.first], pr.evs[sp.second]));
+            st->kernel_ms += ms;
+            st->launches++;
+        }
+        for (auto &sp : pr.rspans) {
+            float ms = 0;
+            HIPCHECK(hipEventElapsedTime(&ms, pr.evs[sp.first], pr.evs[sp.second]));
+            st->reduce_ms += ms;
+        }
+        st->samples += pr.samples;
+    }
+    uint64_t c[32];
+    HIPCHECK(hipMemcpy(c, ds.stats.p, sizeof c, hipMemcpyDeviceToHost));
+    st->queries = c[0] + c[1];
+    st->leaf_queries = c[1];
+    st->attempts = c[2];
+    st->rounds = c[3];
+    st->slow_queries = c[6];
+    st->dark_queries = c[7];
+    st->mid_queries = c[24];
+    if (c[29])
+        st->wave_ms = (double)c[28] * (double)st->launches / (double)c[29] / 1e5; /* 100 MHz clock */
+    if (getenv("PT_PHASE_DUMP")) /* profiling builds (PT_PHASE_TIMING): per-phase wave cycles */
+    {
+        fprintf(stderr, "pt_phases");
+        for (int k = 8; k < 15; k++)
+            fprintf(stderr, " %llu", (unsigned long long)c[k]);
+        for (int k = 16; k < 24; k++)
+            fprintf(stderr, " %llu", (unsigned long long)c[k]);
+        fprintf(stderr, " %llu", (unsigned long long)c[25]); /* whole chunk loop */
+        fprintf(stderr, " %llu %llu", (unsigned long long)c[30], (unsigned long long)c[31]); /* spine queries */
+        fprintf(stderr, "\n");
+    }
+    st->sphere_tests = st->queries * (uint64_t)ds.pending.back().n_spheres;
+    st->plane_tests = st->queries * (uint64_t)ds.pending.back().n_planes;
+    for (auto &pr : ds.pending)
+        for (auto e : pr.evs) (void)hipEventDestroy(e);
+    ds.pending.clear();
+}
+
+/* compact: with a pixel list, pixel k's result goes to fb[3k..3k+2] (else to
+ * its frame position, fb[3 * pixels[k]]) */
+void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream_t stream, pt_render_stats *st,
+                   Timing tm, bool compact = false)
 {
     Generated g;
     DeviceState &ds = prepare(s, p, g);
     const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
+    if (tm == Timing::Sync) {
+        memset(st, 0, sizeof(*st));
+        for (auto &pr : ds.pending) /* a synchronous render reports itself alone */
+            for (auto e : pr.evs) (void)hipEventDestroy(e);
+        ds.pending.clear();
+    }
     if (npix == 0)
         return;
     const int *dpix = nullptr;
@@ -617,19 +701,29 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
         dpix = ds.pixels.p;
     }
     const long long per_pass = pass_samples(p, npix);
-    if (st)
-        memset(st, 0, sizeof(*st));
-    HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 32 * 8, stream));
+    const bool timed = tm != Timing::None;
+    /* the counters restart with the first recorded render */
+    if (!timed || ds.pending.empty())
+        HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 32 * 8, stream));
     hipFunction_t fn = p->order == PT_ORDER_REFERENCE ? ds.strict : ds.fast;
-    std::vector<hipEvent_t> evs;
+    PendingRender pr;
+    pr.n_spheres = g.n_spheres, pr.n_planes = g.n_planes;
+    struct EvGuard /* events of a render that throws before it is recorded */
+    {
+        PendingRender &pr;
+        bool kept = false;
+        ~EvGuard()
+        {
+            if (!kept)
+                for (auto e : pr.evs) (void)hipEventDestroy(e);
+        }
+    } eg{pr};
     auto event = [&]() {
         hipEvent_t e;
         HIPCHECK(hipEventCreate(&e));
+        pr.evs.push_back(e);
         HIPCHECK(hipEventRecord(e, stream));
-        evs.push_back(e);
     };
-    std::vector<std::pair<int, int>> spans; /* (start event, end event) per render launch */
-    std::vector<std::pair<int, int>> rspans;
     for (int s0 = 0; s0 < p->spp; s0 += (int)per_pass) {
         int reduce_mode = 0;
         int nsamp = (int)std::min<long long>(per_pass, p->spp - s0);
@@ -689,78 +783,43 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             float *op = ds.stage.p;
             const int *pp = dpix;
             uint64_t *sp = ds.stats.p; /* counters + the persistent chunk counter (stats[15]) */
-            if (s0 > 0)
-                HIPCHECK(hipMemsetAsync(ds.stats.p + 15, 0, 8, stream));
+            HIPCHECK(hipMemsetAsync(ds.stats.p + 15, 0, 8, stream));
             void *args[] = {&Pp, &ip, &jp, &op, &pp, &sp, &lp};
-            int e0 = (int)evs.size();
-            if (st)
+            int e0 = (int)pr.evs.size();
+            if (timed)
                 event();
             HIPCHECK(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 64 * wpw, 1, 1, 0, stream, args, nullptr));
-            if (st) {
+            if (timed) {
                 event();
-                spans.push_back({e0, e0 + 1});
+                pr.spans.push_back({e0, e0 + 1});
             }
         }
         {
             const float *in = ds.stage.p;
             float *acc = ds.accum.p;
-            const int *pp = dpix;
+            const int *pp = compact ? nullptr : dpix; /* output index: slot (compact) or pixel */
             long long ns = npix;
             int first = s0 == 0, last = s0 + nsamp == p->spp;
             float spp = p->sum_only ? 1.0f : (float)p->spp; /* x / 1 == x: the raw sum */
             void *args[] = {&in, &acc, &fb, &pp, &ns, &nsamp, &first, &last, &spp, &reduce_mode};
             unsigned blocks = (unsigned)((npix + 255) / 256);
-            int e0 = (int)evs.size();
-            if (st)
+            int e0 = (int)pr.evs.size();
+            if (timed)
                 event();
             HIPCHECK(hipModuleLaunchKernel(ds.reduce, blocks, 1, 1, 256, 1, 1, 0, stream, args, nullptr));
-            if (st) {
+            if (timed) {
                 event();
-                rspans.push_back({e0, e0 + 1});
+                pr.rspans.push_back({e0, e0 + 1});
             }
         }
-        if (st)
-            st->samples += (uint64_t)n_items;
+        pr.samples += (uint64_t)n_items;
     }
-    if (st) {
-        HIPCHECK(hipStreamSynchronize(stream));
-        for (auto &sp : spans) {
-            float ms = 0;
-            HIPCHECK(hipEventElapsedTime(&ms, evs[sp.first], evs[sp.second]));
-            st->kernel_ms += ms;
-            st->launches++;
-        }
-        for (auto &sp : rspans) {
-            float ms = 0;
-            HIPCHECK(hipEventElapsedTime(&ms, evs[sp.first], evs[sp.second]));
-            st->reduce_ms += ms;
-        }
-        uint64_t c[32];
-        HIPCHECK(hipMemcpy(c, ds.stats.p, sizeof c, hipMemcpyDeviceToHost));
-        st->queries = c[0] + c[1];
-        st->leaf_queries = c[1];
-        st->attempts = c[2];
-        st->rounds = c[3];
-        st->slow_queries = c[6];
-        st->dark_queries = c[7];
-        st->mid_queries = c[24];
-        if (c[29])
-            st->wave_ms = (double)c[28] * (double)st->launches / (double)c[29] / 1e5; /* 100 MHz clock */
-        if (getenv("PT_PHASE_DUMP")) /* profiling builds (PT_PHASE_TIMING): per-phase wave cycles */
-        {
-            fprintf(stderr, "pt_phases");
-            for (int k = 8; k < 15; k++)
-                fprintf(stderr, " %llu", (unsigned long long)c[k]);
-            for (int k = 16; k < 24; k++)
-                fprintf(stderr, " %llu", (unsigned long long)c[k]);
-            fprintf(stderr, " %llu", (unsigned long long)c[25]); /* whole chunk loop */
-            fprintf(stderr, " %llu %llu", (unsigned long long)c[30], (unsigned long long)c[31]); /* spine queries */
-            fprintf(stderr, "\n");
-        }
-        st->sphere_tests = st->queries * (uint64_t)g.n_spheres;
-        st->plane_tests = st->queries * (uint64_t)g.n_planes;
-        for (auto e : evs) (void)hipEventDestroy(e);
-    }
+    if (!timed)
+        return;
+    eg.kept = true;
+    ds.pending.push_back(std::move(pr));
+    if (tm == Timing::Sync)
+        collect_timings(ds, st);
 }
 
 /* A query module (generate_query) loaded on one device with its own copy of
@@ -1181,7 +1240,34 @@ int pt_render_device(pt_scene *s, const pt_render_params *p, float *fb, void *st
     return guard([&] {
         if (!fb)
             throw Error(PT_ERR_ARG, "null frame buffer");
-        render_device(S(s), p, fb, (hipStream_t)stream, stats);
+        render_device(S(s), p, fb, (hipStream_t)stream, stats, stats ? Timing::Sync : Timing::None);
+        return PT_OK;
+    });
+}
+
+int pt_render_device_timed(pt_scene *s, const pt_render_params *p, float *fb, void *stream)
+{
+    return guard([&] {
+        if (!fb)
+            throw Error(PT_ERR_ARG, "null frame buffer");
+        render_device(S(s), p, fb, (hipStream_t)stream, nullptr, Timing::Deferred);
+        return PT_OK;
+    });
+}
+
+int pt_render_collect(pt_scene *s, int device, pt_render_stats *stats)
+{
+    return guard([&] {
+        if (!stats)
+            throw Error(PT_ERR_ARG, "null stats");
+        SceneImpl &sc = S(s);
+        auto it = sc.devices.find(device);
+        if (it == sc.devices.end() || !it->second) {
+            memset(stats, 0, sizeof(*stats));
+            return PT_OK;
+        }
+        HIPCHECK(hipSetDevice(device));
+        collect_timings(*it->second, stats);
         return PT_OK;
     });
 }
@@ -1194,7 +1280,8 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
         validate(p);
         SceneImpl &sc = S(s);
         HIPCHECK(hipSetDevice(p->device));
-        const size_t n = frame_floats(p);
+        /* a pixel list renders into a compact buffer, pixel k at 3k */
+        const size_t n = p->pixels ? (size_t)std::max<int64_t>(1, p->npixels) * 3 : frame_floats(p);
         DevBuf<float> fb;
         fb.ensure(n);
         struct Free
@@ -1204,16 +1291,11 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
         } fr{fb};
         HIPCHECK(hipMemset(fb.p, 0, n * 4));
         pt_render_stats local;
-        render_device(sc, p, fb.p, nullptr, stats ? stats : &local);
+        render_device(sc, p, fb.p, nullptr, stats ? stats : &local, Timing::Sync, true);
         HIPCHECK(hipDeviceSynchronize());
-        if (!p->pixels) {
-            HIPCHECK(hipMemcpy(rgb_out, fb.p, n * 4, hipMemcpyDeviceToHost));
-        } else {
-            std::vector<float> all(n);
-            HIPCHECK(hipMemcpy(all.data(), fb.p, n * 4, hipMemcpyDeviceToHost));
-            for (int64_t k = 0; k < p->npixels; k++)
-                for (int c = 0; c < 3; c++) rgb_out[3 * k + c] = all[3 * (size_t)p->pixels[k] + c];
-        }
+        const size_t nout = p->pixels ? (size_t)p->npixels * 3 : n;
+        if (nout)
+            HIPCHECK(hipMemcpy(rgb_out, fb.p, nout * 4, hipMemcpyDeviceToHost));
         return PT_OK;
     });
 }
@@ -1579,6 +1661,47 @@ int pt_selftest_math(int device, uint64_t n, uint64_t seed, uint64_t *mismatches
         HIPCHECK(hipMemcpy(mismatches, bad, 24, hipMemcpyDeviceToHost));
         (void)hipFree(bad);
         (void)hipModuleUnload(mod);
+        return PT_OK;
+    });
+}
+
+/* The device's restated glibc float libm on n operand pairs (pt_device.h
+ * pt_selftest_libm): out = n x (atan2f(y, x), asinf(y), logf(x)). */
+int pt_selftest_libm(int device, const float *ops, int64_t n, float *out)
+{
+    return guard([&] {
+        if (!ops || !out || n < 0)
+            throw Error(PT_ERR_ARG, "bad arguments");
+        Generated g;
+        g.source = "#define PT_SELFTEST 1\n" + device_library_source();
+        g.key = "selftest";
+        const std::vector<char> &code = code_object(g);
+        HIPCHECK(hipSetDevice(device));
+        hipModule_t mod;
+        HIPCHECK(hipModuleLoadData(&mod, code.data()));
+        struct Unload
+        {
+            hipModule_t m;
+            ~Unload() { (void)hipModuleUnload(m); }
+        } ul{mod};
+        hipFunction_t fn;
+        HIPCHECK(hipModuleGetFunction(&fn, mod, "pt_selftest_libm"));
+        DevBuf<float> d_ops, d_out;
+        struct Free
+        {
+            DevBuf<float> &a, &b;
+            ~Free() { a.release(), b.release(); }
+        } fr{d_ops, d_out};
+        d_ops.ensure((size_t)std::max<int64_t>(1, 2 * n));
+        d_out.ensure((size_t)std::max<int64_t>(1, 3 * n));
+        if (n) {
+            HIPCHECK(hipMemcpy(d_ops.p, ops, (size_t)n * 8, hipMemcpyHostToDevice));
+            uint64_t nn = (uint64_t)n;
+            void *args[] = {&d_ops.p, &nn, &d_out.p};
+            HIPCHECK(hipModuleLaunchKernel(fn, 1024, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+            HIPCHECK(hipDeviceSynchronize());
+            HIPCHECK(hipMemcpy(out, d_out.p, (size_t)n * 12, hipMemcpyDeviceToHost));
+        }
         return PT_OK;
     });
 }

@@ -29,7 +29,8 @@ from .scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTex
 __all__ = [n for n in dir() if not n.startswith("_")] + ["DeviceScene", "render", "render_device", "prepare"]
 
 ORDERS = {"fast": PT_ORDER_FAST, "reference": PT_ORDER_REFERENCE,
-          "strict": PT_ORDER_REFERENCE}
+          "strict": PT_ORDER_REFERENCE,
+          "group64": PT_ORDER_FAST}  # deprecated name of "fast" (rounds 1-2)
 
 
 class DeviceScene:
@@ -247,8 +248,23 @@ def prepare(scene: DeviceScene, params: RenderParams) -> None:
 
 
 def render_device(scene: DeviceScene, params: RenderParams, fb_ptr: int, stream_ptr: int = 0, stats: bool = False):
-    """Render into device memory fb_ptr (W*H*3 floats) on stream_ptr."""
+    """Render into device memory fb_ptr (W*H*3 floats) on stream_ptr
+    (synchronous when stats are asked for: they need the kernel timings)."""
     st = RenderStats()
     _lib.check(_lib.lib().pt_render_device(scene.handle, ctypes.byref(params), ctypes.c_void_p(fb_ptr),
                                            ctypes.c_void_p(stream_ptr), ctypes.byref(st) if stats else None))
     return st.as_dict() if stats else None
+
+
+def render_device_timed(scene: DeviceScene, params: RenderParams, fb_ptr: int, stream_ptr: int = 0) -> None:
+    """render_device without a host wait: its kernel timings and counters are
+    kept on the device until render_collect (pt_render_device_timed)."""
+    _lib.check(_lib.lib().pt_render_device_timed(scene.handle, ctypes.byref(params), ctypes.c_void_p(fb_ptr),
+                                                 ctypes.c_void_p(stream_ptr)))
+
+
+def render_collect(scene: DeviceScene, device: int = 0) -> dict:
+    """Summed statistics of the timed renders since the last collect (waits for them)."""
+    st = RenderStats()
+    _lib.check(_lib.lib().pt_render_collect(scene.handle, int(device), ctypes.byref(st)))
+    return st.as_dict()

@@ -88,6 +88,8 @@ SIGNATURES = {
     "pt_matrix_concat": (None, [_FP, _FP, _FP]),
     "pt_render": (_I, [_P, ctypes.POINTER(RenderParams), _P, ctypes.POINTER(RenderStats)]),
     "pt_render_device": (_I, [_P, ctypes.POINTER(RenderParams), _P, _P, ctypes.POINTER(RenderStats)]),
+    "pt_render_device_timed": (_I, [_P, ctypes.POINTER(RenderParams), _P, _P]),
+    "pt_render_collect": (_I, [_P, _I, ctypes.POINTER(RenderStats)]),
     "pt_render_adaptive": (_I, [_P, ctypes.POINTER(RenderParams), ctypes.POINTER(AdaptiveParams), _P,
                                 ctypes.POINTER(RenderStats)]),
     "pt_prepare": (_I, [_P, ctypes.POINTER(RenderParams)]),
@@ -98,6 +100,7 @@ SIGNATURES = {
     "pt_scene_set_lane_scatter": (_I, [_P, _I]),
     "pt_scene_kernel_key": (ctypes.c_char_p, [_P, _I]),
     "pt_selftest_math": (_I, [_I, ctypes.c_uint64, ctypes.c_uint64, _P]),
+    "pt_selftest_libm": (_I, [_I, _P, ctypes.c_int64, _P]),
     "pt_query_spans": (_I, [_P, _I, _P, ctypes.c_int64, _I, _P, _P, _I]),
     "pt_tex_eval": (_I, [_P, _I, _P, ctypes.c_int64, _P, _P, _I]),
     "pt_query_compile": (_I, [_P, _I, _I]),
@@ -193,3 +196,13 @@ def write_bmp(path: str, rgb: np.ndarray, count: int = 1) -> None:
     rgb = np.ascontiguousarray(rgb, dtype=np.float32)
     h, w = rgb.shape[:2]
     check(lib().pt_write_bmp(path.encode(), rgb.ctypes.data, w, h, count))
+
+
+def selftest_libm(ops, device: int = 0):
+    """The device's restated atan2f / asinf / logf (pt_selftest_libm) on operand
+    pairs ops (n x 2 float32: y, x): returns n x 3 (atan2f(y, x), asinf(y), logf(x))."""
+    import numpy as np
+    ops = np.ascontiguousarray(ops, dtype=np.float32).reshape(-1, 2)
+    out = np.zeros((len(ops), 3), dtype=np.float32)
+    check(lib().pt_selftest_libm(device, ops.ctypes.data, len(ops), out.ctypes.data))
+    return out

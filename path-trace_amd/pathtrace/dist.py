@@ -65,7 +65,7 @@ class RankFrame:
         from . import make_params
         if split not in ("samples", "tiles"):
             raise ValueError("split must be 'samples' or 'tiles'")
-        self.ds, self.rank, self.world, self.spp = ds, rank, world, spp
+        self.ds, self.rank, self.world, self.spp, self.device = ds, rank, world, spp, device
         self.by_samples = world > 1 and split == "samples"
         mine = rank_pixels(width, height, rank, 1 if self.by_samples else world)
         if subset is not None:
@@ -90,6 +90,16 @@ class RankFrame:
         """this rank's contribution into the zeroed device frame at fb_ptr"""
         from . import render_device
         return render_device(self.ds, self.params, fb_ptr, stream_ptr, stats=stats)
+
+    def render_async(self, fb_ptr, stream_ptr=0):
+        """render() queued on the stream without a host wait; collect() sums
+        the timings and counters of every render_async since the last one"""
+        from . import render_device_timed
+        render_device_timed(self.ds, self.params, fb_ptr, stream_ptr)
+
+    def collect(self):
+        from . import render_collect
+        return render_collect(self.ds, self.device)
 
     def finish(self, fb):
         """after the sum-reduce to rank 0: the frame of means (torch tensor, in place)"""

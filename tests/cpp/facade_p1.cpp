@@ -143,6 +143,30 @@ int main(int argc, char **argv)
             fclose(f);
             return 0;
         }
+        if (!strcmp(argv[1], "tracepixel") && argc == 7) {
+            /* the reference demo's per-pixel call (src/test.cpp:450, 503) */
+            const int W = atoi(argv[2]), H = atoi(argv[3]), spp = atoi(argv[4]), depth = atoi(argv[5]);
+            std::unique_ptr<SpanIterator> spanIterator(world->makeSpanIterator());
+            std::vector<Color> img;
+            FrameEngine engine; /* run seed 0x5EED, fast order: Renderer::render's defaults */
+            for (int y = 0; y < H; y++)
+                for (int x = 0; x < W; x++)
+                    img.push_back(tracePixel(*spanIterator, x, y, W, H, spp, depth, (float)W, (float)H,
+                                             (float)(2 * (W < H ? W : H)), engine));
+            /* the demo's exact call shape (global engine, int screen sizes) and
+             * a block corner one past the right edge: they run */
+            const int ScreenWidth = W, ScreenHeight = H;
+            Color c = tracePixel(*spanIterator, W, 0, ScreenWidth, ScreenHeight, spp, depth, ScreenWidth,
+                                 ScreenHeight, (ScreenWidth < ScreenHeight ? ScreenWidth : ScreenHeight) * 2);
+            if (!(c.x == c.x))
+                return 7;
+            FILE *f = fopen(argv[6], "wb");
+            if (!f)
+                return 5;
+            fwrite(img.data(), sizeof(Color), img.size(), f);
+            fclose(f);
+            return 0;
+        }
         Renderer renderer(world.get());
         if (!strcmp(argv[1], "key") && argc == 3) {
             printf("%s\n", pt_scene_kernel_key(renderer.handle(), atoi(argv[2])));

@@ -1,0 +1,66 @@
+"""bench.py's N > 1 code path rehearsed on one GPU (tests for VERDICT r3 #4):
+two ranks under torch.distributed.run with the gloo backend (the frame
+reduced through host memory) run exactly the multi-GPU step -- RankFrame's
+share, the asynchronous timed render, the reduce, rank 0's division by spp,
+the max-over-ranks timing, the roofline divided over ranks, the CPU leg on
+rank 0 -- and the reduced frame equals the one-rank frame."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _bench(args, nproc, tmp_path, name):
+    frame = str(tmp_path / (name + ".npy"))
+    cmd = [sys.executable, "-u"]
+    if nproc > 1:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())]
+    cmd += [os.path.join(ROOT, "bench.py"), "--gpus", str(nproc)] + args + ["--dump-frame", frame]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints one JSON line
+    return json.loads(lines[0]), np.load(frame)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", ["samples", "tiles"])
+def test_bench_two_ranks_gloo(tmp_path, split):
+    common = ["--config", "C3", "--spp", "64", "--steps", "1", "--warmup", "0", "--cpu-pixels", "64"]
+    one, f1 = _bench(common + ["--no-cpu"], 1, tmp_path, "one")
+    two, f2 = _bench(common + ["--backend", "gloo", "--split", split], 2, tmp_path, "two")
+    assert two["n_gpus"] == 2 and two["steps"] == 1
+    assert "gloo reduce" in two["config"]["sharding"]
+    assert ("spp split" in two["config"]["sharding"]) == (split == "samples")
+    assert two["samples_per_step"] == one["samples_per_step"] == 1920 * 1080 * 64
+    # the same frame: the same span queries in total, split over the ranks
+    assert two["queries_per_sample"] == pytest.approx(one["queries_per_sample"], rel=1e-9)
+    # roofline: each rank's launches carry half the work; the kernel time is the max over ranks
+    rf = two["roofline"]
+    assert rf["kernel"] == "pt_render_fast" and rf["avg_launch_ms"] > 0
+    ops_launch = rf["ops_per_query"] * two["queries_per_sample"] * two["samples_per_step"] / 2
+    assert rf["achieved"] == pytest.approx(ops_launch / (rf["avg_launch_ms"] * 1e-3) / 1e12, rel=2e-3)
+    # rank 0 ran the CPU leg after the timed region, on the reduced frame
+    assert two["cpu_baseline"]["kind"] in ("reference", "port") and two["cpu_baseline"]["value"] > 0
+    assert max(two["rmse_vs_cpu_ref"]) < 1e-3
+    if split == "tiles":  # disjoint tiles: x + 0.0 == x
+        np.testing.assert_array_equal(f2.view(np.uint32), f1.view(np.uint32))
+    else:  # the ranks' partial sums change the association only
+        rmse = np.sqrt(np.mean((f2.astype(np.float64) - f1) ** 2, axis=(0, 1)))
+        assert rmse.max() <= 1e-6, rmse

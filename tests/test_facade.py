@@ -50,6 +50,21 @@ def test_facade_render_bitexact(facade_bin, tmp_path):
 
 
 @pytest.mark.gpu
+def test_facade_trace_pixel_bitexact(facade_bin, tmp_path):
+    """tracePixel(*spanIterator, x, y, W, H, spp, depth, sw, sh, dist, engine) per
+    pixel -- the reference demo's call (src/test.cpp:450) against the facade --
+    gives Renderer::render's frame bit for bit (same run seed, fast order)."""
+    W, H, spp, depth = 24, 16, 4, 8
+    out = str(tmp_path / "tp.bin")
+    r = subprocess.run([facade_bin, "tracepixel", str(W), str(H), str(spp), str(depth), out],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(out, dtype=np.float32).reshape(-1, 3)
+    want = pt.render(scenes.scene_p1(), W, H, spp, depth).reshape(-1, 3)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
 def test_facade_span_iterator_matches_oracle(facade_bin, tmp_path):
     """world->makeSpanIterator() through the facade (pt_query_spans): init(Ray)
     / isAtEnd / operator* / next give the reference's span lists, bit for bit

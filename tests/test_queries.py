@@ -9,8 +9,8 @@
   pt_tex_eval     Texture::getColor / getFloat (include/texture.h:13-18) of
                   every texture of the texture zoos at 2048 points, against the
                   reference's lookups (tests/golden/tex_eval.npz): bit for bit
-                  for IEEE-exact textures; the transcendental zoo (atan2f/asinf/
-                  logf, whose last ulp may differ from glibc) to a tolerance."""
+                  for every texture, the transcendental zoo included (atan2f/asinf/
+                  logf restated from glibc on the device)."""
 import os
 
 import numpy as np
@@ -67,9 +67,6 @@ def test_tex_eval_matches_reference(built, tmp_path, name):
         rgb, val = ds.tex_eval(k, z["points"])
         got[k, :, :3], got[k, :, 3] = rgb, val
     same = got.view(np.uint32) == want.view(np.uint32)
-    if name == "texture_zoo":
-        assert same.all(), "%d of %d lookups differ" % ((~same).sum(), same.size)
-    else:
-        # spherical maps / log filter: the device's atan2/asin/log may differ from glibc's
-        # atan2f/asinf/logf in the last ulp, which can move a texel; nearly all stay exact
-        assert same.mean() >= 0.99, same.mean()
+    # bit for bit, the transcendental zoo too: the spherical maps' atan2f / asinf
+    # and the log filter's logf are glibc's algorithms restated (tests/test_libm.py)
+    assert same.all(), "%d of %d lookups differ" % ((~same).sum(), same.size)

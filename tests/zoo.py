@@ -111,7 +111,9 @@ RENDER_CASES = [
     ("tex", "texture_zoo", 32, 24, 3, 5),
     ("texm", "texture_transc_zoo", 32, 24, 3, 5),
 ]
-EXACT_CASES = [c for c in RENDER_CASES if c[0] != "texm"]
+# every case bit for bit: the spherical map's atan2f / asinf and LogTexture's
+# logf are glibc's algorithms restated on the device (tests/test_libm.py)
+EXACT_CASES = list(RENDER_CASES)
 # (builder, depth) of scenes only the GPU tests render (against the oracle, no goldens)
 GPU_ONLY_CASES = [("union_zoo", 6)]
 

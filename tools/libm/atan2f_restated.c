@@ -1,4 +1,14 @@
-/* fdlibm-style float atan / atan2 restated (feasibility check against glibc 2.35) */
+/* fdlibm float atan / atan2 restated (the device's libm_atanf / libm_atan2f,
+ * pt_device.h) and checked against this host's glibc 2.35 atanf / atan2f.
+ *
+ * Algorithm and constants: Sun fdlibm s_atan.c / e_atan2.c as converted to
+ * float (e_atan2f.c, s_atanf.c) and shipped in glibc sysdeps/ieee754/flt-32:
+ *   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ *   Developed at SunPro, a Sun Microsystems, Inc. business.
+ *   Permission to use, copy, modify, and distribute this software is freely
+ *   granted, provided that this notice is preserved.
+ *   (Conversion to float by Ian Lance Taylor, Cygnus Support.)
+ *   gcc -O2 -ffp-contract=off tools/libm/atan2f_restated.c -lm && ./a.out */
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -38,11 +48,14 @@ static float my_atan2f(float y, float x) {
     int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
     if (iy == 0) { switch (m) { case 0: case 1: return y; case 2: return pi; default: return -pi; } }
     if (ix == 0) return hy < 0 ? -pi_o_2 : pi_o_2;
-    if (ix == 0x7f800000) { /* not needed for unit vectors */ return atan2f(y, x); }
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) { switch (m) { case 0: return pi_o_4; case 1: return -pi_o_4; case 2: return 3.0f * pi_o_4; default: return -3.0f * pi_o_4; } }
+        switch (m) { case 0: return 0.0f; case 1: return -0.0f; case 2: return pi; default: return -pi; }
+    }
     if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 : pi_o_2;
     int k = (iy - ix) >> 23; float z;
-    if (k > 26) { z = pi_o_2 + 0.5f * pi_lo; m &= 1; }
-    else if (k < -26 && hx < 0) z = 0.0f;
+    if (k > 60) z = pi_o_2 + 0.5f * pi_lo;      /* glibc flt-32: 60, and no m &= 1 (FreeBSD: 26, m &= 1) */
+    else if (k < -60 && hx < 0) z = 0.0f;
     else z = my_atanf(fabsf(y / x));
     switch (m) { case 0: return z; case 1: return -z; case 2: return pi - (z - pi_lo); default: return (z - pi_lo) - pi; }
 }
@@ -57,4 +70,29 @@ int main(void) {
         if (my_atanf(t) != atanf(t)) bt++;
     }
     printf("atan2f mismatches %ld of %ld, atanf %ld\n", ba, n, bt);
+    /* the branches uniform operands in [-1, 1] miss: large exponent gaps both
+     * ways (k > 26, k < -26 with x < 0), signed zeros, infinities, NaN */
+    long be = 0, ne = 0;
+    const float mant[] = {1.0f, 1.5f, 1.25f, 1.9999999f, 1.3333334f};
+    for (int ey = -140; ey <= 127; ey++)
+        for (int ex = -140; ex <= 127; ex += 3)
+            for (int a = 0; a < 5; a++)
+                for (int b = 0; b < 5; b++)
+                    for (int sg = 0; sg < 4; sg++) {
+                        float y = ldexpf(mant[a], ey), x = ldexpf(mant[b], ex);
+                        if (sg & 1) y = -y;
+                        if (sg & 2) x = -x;
+                        float m = my_atan2f(y, x), g = atan2f(y, x);
+                        ne++;
+                        if (bits(m) != bits(g)) { if (be < 5) printf("edge mismatch y=%a x=%a mine=%a glibc=%a\n", y, x, m, g); be++; }
+                    }
+    const float sp[] = {0.0f, -0.0f, 1.0f, -1.0f, 0x1p-30f, -0x1p-30f, 0x1p-149f, -0x1p-149f, INFINITY, -INFINITY, NAN};
+    for (int i = 0; i < 11; i++)
+        for (int j = 0; j < 11; j++) {
+            float m = my_atan2f(sp[i], sp[j]), g = atan2f(sp[i], sp[j]);
+            ne++;
+            if (bits(m) != bits(g) && !(m != m && g != g)) { if (be < 10) printf("special mismatch y=%a x=%a mine=%a glibc=%a\n", sp[i], sp[j], m, g); be++; }
+        }
+    printf("atan2f edge operands: %ld mismatches of %ld\n", be, ne);
+    return (ba || bt || be) ? 1 : 0;
 }
