@@ -346,6 +346,21 @@ __device__ __forceinline__ int mask_sel(u64 m, int a, int b)
     asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
     return r;
 }
+/* v + this lane's bit of the uniform mask m: one v_addc with m as carry-in */
+__device__ __forceinline__ int add_lane_bit(int v, u64 m)
+{
+    int r;
+    u64 co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(v), "s"(m));
+    return r;
+}
+/* 0 where this lane's bit of the uniform mask m is set, else v */
+__device__ __forceinline__ int zero_if(u64 m, int v)
+{
+    int r;
+    asm("v_cndmask_b32_e64 %0, %1, 0, %2" : "=v"(r) : "v"(v), "s"(m));
+    return r;
+}
 /* base + set bits of the uniform mask m in the lanes below this one (v_mbcnt) */
 __device__ __forceinline__ int mbcnt(u64 m, int base)
 {
@@ -518,15 +533,34 @@ __device__ __forceinline__ int sep(const PS &ps, int x, int y)
  * stays valid.  (y starting at or before x0 -- B covering x, or the :124-130
  * quirk's inverted span -- keeps the strict rule.)  Intersection nodes keep
  * the strict rule: separation there means an empty intersection. */
+/* A positive span that ends before EPS (a ray leaving the surface it starts
+ * on) is inert: every span the merges above derive from it ends before EPS
+ * too -- a Union merge with a span y that reaches EPS ends at y's end with
+ * y's ref and starts before EPS like y (src/union.cpp:105-132), a Difference
+ * only cuts it (its pieces, and the :124-130 quirk's inverted span, end at or
+ * before its end), and the B spans a Difference consumes while passing it end
+ * before it, i.e. before any later A span that the checks keep apart from it.
+ * The scan (path-trace.h:66-100) skips spans ending before EPS, so the pair
+ * checks may ignore it (the first-hit choice never takes it: its t1 < EPS).
+ * Only positives: a B-side span that ends before EPS can still trigger the
+ * quirk on the A span it overlaps. */
 enum { NODE_ISECT = 0, NODE_UNION = 1, NODE_DIFF = 2 };
+#ifndef PT_INERT
+#define PT_INERT 1
+#endif
+template <class PS>
+__device__ __forceinline__ int inert(const PS &ps, int x)
+{
+    return PT_INERT ? ps.live[x] & (ps.t1[x] < EPS) : 0;
+}
 template <int KIND, class PS>
 __device__ __forceinline__ int pair_ok(const PS &ps, int x, int y)
 {
     int ok = sep(ps, x, y);
     if (KIND == NODE_UNION)
-        ok |= (ps.t0[x] >= EPS) & (ps.t0[y] >= EPS) & (ps.t0[x] != ps.t0[y]);
+        ok |= ((ps.t0[x] >= EPS) & (ps.t0[y] >= EPS) & (ps.t0[x] != ps.t0[y])) | inert(ps, x) | inert(ps, y);
     if (KIND == NODE_DIFF)
-        ok |= (ps.t0[x] >= EPS) & (ps.t0[y] > ps.t0[x]);
+        ok |= ((ps.t0[x] >= EPS) & (ps.t0[y] > ps.t0[x])) | inert(ps, x);
     return ok;
 }
 
@@ -1759,9 +1793,9 @@ __device__ __forceinline__ void cadd(u64 &c, u32 v)
 /* LCG jumps in LDS, shared by the workgroup's waves: j3[l] = (A, G * inc) of
  * 3l draws (attempt l of a round, lane l in attempt-major rounds; k < 8: the
  * offset of a lane-major round's k-th attempt), j24[l] = the same for 24l
- * draws (lane l's first attempt, 8l, in a lane-major round).  Read through
- * volatile loads where a round needs them: hoisted out of the burst loop
- * they would be held in registers and spilled to scratch. */
+ * draws (lane l's first attempt, 8l, in a lane-major round).  Read where a
+ * round needs them: hoisted out of the burst loop they would be held in
+ * registers and spilled to scratch. */
 struct JumpLds
 {
     const u64 (*j3)[2];
@@ -1769,9 +1803,46 @@ struct JumpLds
 };
 __device__ __forceinline__ void jread(const u64 (*t)[2], int i, u64 &A, u64 &G)
 {
-    const volatile u64 *p = t[i];
-    A = p[0];
-    G = p[1];
+    /* an index the compiler cannot see through: the load stays in the round
+     * (a volatile load would lose the LDS address space and go through flat) */
+    asm volatile("" : "+v"(i));
+    A = t[i][0];
+    G = t[i][1];
+}
+/* A burst-uniform struct parked in LDS, padded to whole 16-byte words so
+ * that it is read with ds_read_b128 (a struct of floats is only 4-byte
+ * aligned: the compiler would read it two words at a time). */
+template <class T>
+struct alignas(16) LdsBox
+{
+    static constexpr int N = (int)((sizeof(T) + 15) / 16);
+    float4 w[N];
+};
+template <class T>
+__device__ __forceinline__ T lds_get(const LdsBox<T> &b)
+{
+    union
+    {
+        float4 w[LdsBox<T>::N];
+        T t;
+    } u;
+#pragma unroll
+    for (int i = 0; i < LdsBox<T>::N; i++)
+        u.w[i] = b.w[i];
+    return u.t;
+}
+template <class T>
+__device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
+{
+    union
+    {
+        float4 w[LdsBox<T>::N];
+        T t;
+    } u;
+    u.t = t;
+#pragma unroll
+    for (int i = 0; i < LdsBox<T>::N; i++)
+        b.w[i] = u.w[i];
 }
 #ifndef PT_LANE_MAJOR
 #define PT_LANE_MAJOR 1 /* deferred rounds: lane l evaluates attempts 8l..8l+7 (one chained stream) */
@@ -2062,10 +2133,10 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     int fails = 0, reason = -1;
     /* the burst origin's primitive contexts, shared by every pass of the burst
      * (and, in registers, by the generation rounds' dark test) */
-    typename S::Root::Ctx *const cxp = (typename S::Root::Ctx *)L.ctx;
+    LdsBox<typename S::Root::Ctx> *const cxp = (LdsBox<typename S::Root::Ctx> *)L.ctx;
     typename S::Root::Ctx c0;
     S::Root::prep(c0, hit, e);
-    *cxp = c0;
+    lds_put(*cxp, c0);
     /* The burst's leaf children form one run of the fast order (oracle.cpp
      * ORDER_FAST): the run's non-zero terms are dealt round-robin to 64 lane
      * sums (lsum; the k-th one to lane k mod 64), which are added into retval
@@ -2191,7 +2262,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         ta += __popcll(ap.A[h]);
                         tk += __popcll(K[k + h]);
                         Aor |= ap.A[h];
-                        tf = mask_sel(ap.A[h], 0, tf + lane_bit(ap.F[h]));
+                        tf = zero_if(ap.A[h], add_lane_bit(tf, ap.F[h]));
                     }
                 }
                 /* ring entries, numbered in child order */
@@ -2205,7 +2276,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         ring[slot & (PT_RCAP - 1)] = make_float4(__uint_as_float((u32)s_lane),
                                                                  __uint_as_float((u32)(s_lane >> 32)),
                                                                  __int_as_float(k), 0.0f);
-                    slot += lane_bit(K[k]);
+                    slot = add_lane_bit(slot, K[k]);
                 }
                 /* failures after the round's last accepted attempt (lane L,
                  * then every lane above it); none accepted: all of them */
@@ -2372,7 +2443,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
         auto fast_lane = [&](int pos, float4 en) -> bool {
             const V3 dir = mk(en.x, en.y, en.z);
             PT_MARK(8);
-            const typename S::Root::Ctx ctx = *cxp;
+            const typename S::Root::Ctx ctx = lds_get(*cxp);
             PrimSpans<S::Root::HI> ps;
             PT_MARK(9);
             S::Root::span(ps, ctx, mkray(dir), e);
@@ -2428,7 +2499,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     const int pos = slot_pos(slowq[(s_head + lane) & (PT_SCAP - 1)]);
                     const float4 en = ring[pos & (PT_RCAP - 1)];
                     const V3 dir = mk(en.x, en.y, en.z);
-                    const typename S::Root::Ctx ctx = *cxp;
+                    const typename S::Root::Ctx ctx = lds_get(*cxp);
                     float t;
                     u32 ref;
                     bool ex;
@@ -2513,7 +2584,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         if (clear_on) {
                             PT_MARK(16);
                             const V3 dir = mk(en.x, en.y, en.z);
-                            const typename S::Root::Ctx ctx = *cxp;
+                            const typename S::Root::Ctx ctx = lds_get(*cxp);
                             const Ray q = mkray(dir);
                             const u64 CM = S::Root::template clear_mask<Emissive<S>, true>(ctx, q, e);
                             PrimSpans<S::Root::HI> ps;
@@ -3366,7 +3437,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                                              const PtLaunch &lp)
 {
     __shared__ Frame stk[PT_WPW][MAXD + 1];
-    __shared__ typename S::Root::Ctx xbuf[PT_WPW];
+    __shared__ LdsBox<typename S::Root::Ctx> xbuf[PT_WPW];
     __shared__ float4 rbuf[PT_WPW][PT_RCAP];
     __shared__ unsigned char sbuf[PT_WPW][PT_SCAP];
     __shared__ unsigned char mbuf[PT_WPW][PT_SCAP];
@@ -3580,7 +3651,7 @@ template <class S, int MAXD>
 __device__ constexpr int min_workgroups()
 {
     constexpr int lds = PT_WPW * ((MAXD + 1) * (int)sizeof(Frame) + 16 * PT_RCAP + 2 * PT_SCAP +
-                                  (int)sizeof(Counters) + (int)sizeof(typename S::Root::Ctx) + 64 * 16) +
+                                  (int)sizeof(Counters) + (int)sizeof(LdsBox<typename S::Root::Ctx>) + 64 * 16) +
                         2 * 64 * 16;
     constexpr int alloc = (lds + 1279) / 1280 * 1280; /* gfx950 LDS allocation unit (measured) */
     constexpr int n = 160 * 1024 / alloc;

@@ -72,10 +72,12 @@ struct SceneImpl
     int lane_walk = 0;             /* register frames of the per-lane scatter-free tree walk (0 = off) */
     int lane_scatter = 0;          /* per-lane walk of whole trees, scatter loops included */
     std::map<int, std::unique_ptr<DeviceState>> devices;
+    std::shared_ptr<struct QueryCache> qcache; /* loaded query modules (runtime.cpp) */
     std::string last_key;
     void clear()
     {
         images.clear(), textures.clear(), materials.clear(), objects.clear();
+        qcache.reset(); /* its modules hold copies of the old images */
         root = -1;
         default_tex[0] = default_tex[1] = -1;
     }

@@ -823,41 +823,44 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
 }
 
 /* A query module (generate_query) loaded on one device with its own copy of
- * the parameters and images; everything is released with it. */
+ * the parameters and images; everything is released with it.  A scene keeps
+ * the modules it has served (SceneImpl::qcache): a scene only grows, so a
+ * module whose source key, parameters and image slots match is the same
+ * module, and the facade's per-ray / per-point virtuals (SpanIterator::init,
+ * Texture::getColor) reuse it instead of loading a code object per call. */
 struct QueryModule
 {
     int device;
     hipModule_t mod = nullptr;
+    std::vector<float> params;
+    std::vector<int> image_ids;
     DevBuf<float> P;
     DevBuf<PtImageDev> imgs;
     std::vector<DevBuf<float>> img_data;
-    std::vector<void *> scratch;
-    QueryModule(SceneImpl &s, const Generated &g, int dev) : device(dev)
+    QueryModule(SceneImpl &s, const Generated &g, int dev) : device(dev), params(g.params), image_ids(g.image_ids)
     {
         const std::vector<char> &code = code_object(g);
         HIPCHECK(hipSetDevice(device));
         HIPCHECK(hipModuleLoadData(&mod, code.data()));
-        P.ensure(g.params.size());
-        HIPCHECK(hipMemcpy(P.p, g.params.data(), g.params.size() * 4, hipMemcpyHostToDevice));
-        img_data.resize(g.image_ids.size());
-        std::vector<PtImageDev> desc(g.image_ids.size() + 1);
-        for (size_t k = 0; k < g.image_ids.size(); k++) {
-            const ImageRec &im = s.images.at(g.image_ids[k]);
-            img_data[k].ensure(im.rgba.size());
-            HIPCHECK(hipMemcpy(img_data[k].p, im.rgba.data(), im.rgba.size() * 4, hipMemcpyHostToDevice));
-            desc[k].data = img_data[k].p;
-            desc[k].w = (uint32_t)im.w;
-            desc[k].h = (uint32_t)im.h;
+        try {
+            P.ensure(g.params.size());
+            HIPCHECK(hipMemcpy(P.p, g.params.data(), g.params.size() * 4, hipMemcpyHostToDevice));
+            img_data.resize(g.image_ids.size());
+            std::vector<PtImageDev> desc(g.image_ids.size() + 1);
+            for (size_t k = 0; k < g.image_ids.size(); k++) {
+                const ImageRec &im = s.images.at(g.image_ids[k]);
+                img_data[k].ensure(im.rgba.size());
+                HIPCHECK(hipMemcpy(img_data[k].p, im.rgba.data(), im.rgba.size() * 4, hipMemcpyHostToDevice));
+                desc[k].data = img_data[k].p;
+                desc[k].w = (uint32_t)im.w;
+                desc[k].h = (uint32_t)im.h;
+            }
+            imgs.ensure(desc.size());
+            HIPCHECK(hipMemcpy(imgs.p, desc.data(), desc.size() * sizeof(PtImageDev), hipMemcpyHostToDevice));
+        } catch (...) { /* the destructor does not run for a half-built object */
+            release();
+            throw;
         }
-        imgs.ensure(desc.size());
-        HIPCHECK(hipMemcpy(imgs.p, desc.data(), desc.size() * sizeof(PtImageDev), hipMemcpyHostToDevice));
-    }
-    void *alloc(size_t bytes)
-    {
-        void *q = nullptr;
-        HIPCHECK(hipMalloc(&q, bytes ? bytes : 4));
-        scratch.push_back(q);
-        return q;
     }
     hipFunction_t fn(const char *name)
     {
@@ -865,16 +868,75 @@ struct QueryModule
         HIPCHECK(hipModuleGetFunction(&f, mod, name));
         return f;
     }
-    ~QueryModule()
+    void release()
     {
-        for (void *q : scratch) (void)hipFree(q);
         P.release(), imgs.release();
         for (auto &b : img_data) b.release();
         if (mod)
             (void)hipModuleUnload(mod);
+        mod = nullptr;
+    }
+    ~QueryModule()
+    {
+        int prev = 0;
+        if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(device) == hipSuccess) {
+            release();
+            (void)hipSetDevice(prev);
+        }
     }
 };
 
+/* Restores the calling thread's current HIP device on scope exit. */
+struct DeviceGuard
+{
+    int prev = -1;
+    DeviceGuard() { (void)hipGetDevice(&prev); }
+    ~DeviceGuard()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+/* scratch device memory of one query call */
+struct Scratch
+{
+    std::vector<void *> v;
+    void *alloc(size_t bytes)
+    {
+        void *q = nullptr;
+        HIPCHECK(hipMalloc(&q, bytes ? bytes : 4));
+        v.push_back(q);
+        return q;
+    }
+    ~Scratch()
+    {
+        for (void *q : v) (void)hipFree(q);
+    }
+};
+
+} // namespace
+
+/* the scene's loaded query modules, by (source key, device) */
+struct QueryCache
+{
+    std::map<std::pair<std::string, int>, std::unique_ptr<QueryModule>> mods;
+};
+
+namespace
+{
+QueryModule &query_module(SceneImpl &s, const Generated &g, int device)
+{
+    if (!s.qcache)
+        s.qcache = std::shared_ptr<QueryCache>(new QueryCache);
+    std::unique_ptr<QueryModule> &q = s.qcache->mods[{g.key, device}];
+    if (q && (q->params != g.params || q->image_ids != g.image_ids))
+        q.reset();
+    if (!q)
+        q.reset(new QueryModule(s, g, device));
+    HIPCHECK(hipSetDevice(device));
+    return *q;
+}
 } // namespace
 
 } // namespace pt
@@ -1563,10 +1625,12 @@ int pt_query_spans(pt_scene *s, pt_id obj, const float *rays, int64_t n, int max
             return PT_OK;
         static_assert(sizeof(pt_span) == 40, "pt_span is ten 4-byte words");
         Generated g = generate_query(sc, obj, -1);
-        QueryModule q(sc, g, device);
-        float *dr = (float *)q.alloc((size_t)n * 24);
-        float *dout = (float *)q.alloc((size_t)n * std::max(1, max_spans) * 40);
-        int *dc = (int *)q.alloc((size_t)n * 4);
+        DeviceGuard dg;
+        QueryModule &q = query_module(sc, g, device);
+        Scratch sm;
+        float *dr = (float *)sm.alloc((size_t)n * 24);
+        float *dout = (float *)sm.alloc((size_t)n * std::max(1, max_spans) * 40);
+        int *dc = (int *)sm.alloc((size_t)n * 4);
         HIPCHECK(hipMemcpy(dr, rays, (size_t)n * 24, hipMemcpyHostToDevice));
         const float *Pp = q.P.p;
         const PtImageDev *ip = q.imgs.p;
@@ -1601,9 +1665,11 @@ int pt_tex_eval(pt_scene *s, pt_id tex, const float *points, int64_t n, float *r
         if (n == 0)
             return PT_OK;
         Generated g = generate_query(sc, -1, tex);
-        QueryModule q(sc, g, device);
-        float *dp = (float *)q.alloc((size_t)n * 12), *dc = (float *)q.alloc((size_t)n * 12);
-        float *dv = (float *)q.alloc((size_t)n * 4);
+        DeviceGuard dg;
+        QueryModule &q = query_module(sc, g, device);
+        Scratch sm;
+        float *dp = (float *)sm.alloc((size_t)n * 12), *dc = (float *)sm.alloc((size_t)n * 12);
+        float *dv = (float *)sm.alloc((size_t)n * 4);
         HIPCHECK(hipMemcpy(dp, points, (size_t)n * 12, hipMemcpyHostToDevice));
         const float *Pp = q.P.p;
         const PtImageDev *ip = q.imgs.p;
