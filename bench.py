@@ -42,7 +42,7 @@ VALU_PEAK_TOPS = 78.6  # 256 CU x 128 FP32 lanes/clk x 2.4 GHz, no FMA (contract
 OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 614.78, "C5": 554.13}
 # Counter evidence of this same command (tools/pmc_bench.sh: rocprofv3 --pmc
 # passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 + WRITE_SIZE)
-PMC_JSON = os.path.join(ROOT, "profiles", "round3", "pmc_bench_%s.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "round4", "pmc_bench_%s.json")
 # bounded CPU samples at full spp on the box's per-GPU CPU share (16 threads):
 # BASELINE.md's 4096 hashed pixels (C3: ~60 s), fewer where a pixel costs more
 CPU_PIXELS = {"C1": 4096, "C2": 512, "C3": 4096, "C4": 1024, "C5": 32768}
@@ -139,8 +139,12 @@ def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps, within=None):
         # the reference pool spawns hardware_concurrency() threads (src/test.cpp:204); the
         # GPU box asks for its per-GPU CPU share only, so the whole host is a projection
         # (pixels are independent: the pool scales linearly until memory bandwidth binds)
-        out["all_host_cpus_projected"] = {"value": round(value * host / threads, 5), "cores": host,
-                                          "how": "linear from the measured %d threads (not measured)" % threads}
+        out["all_host_cpus_projected"] = {
+            "value": round(value * host / threads, 5), "cores": host,
+            "how": "linear from the measured %d threads (not measured)" % threads,
+            "why_not_measured": "the GPU box gives each GPU job a %d-thread CPU share (OMP_NUM_THREADS); the "
+                                "reference pool's hardware_concurrency() threads (src/test.cpp:204) would take the "
+                                "other GPUs' shares of this %d-CPU host" % (threads, host)}
     if frame_qps:
         out["frame_queries_per_sample"] = round(frame_qps, 2)
         out["value_rescaled_to_frame"] = round(value * qps / frame_qps, 5)

@@ -564,6 +564,12 @@ __device__ __forceinline__ int pair_ok(const PS &ps, int x, int y)
     return ok;
 }
 
+/* Selects every primitive (each_sel) */
+struct AllPrims
+{
+    __device__ static constexpr bool take(int) { return true; }
+};
+
 /* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r.  Branch-free:
  * t0/t1 are computed on every lane (dead lanes' values are never read), with
  * one wave-uniform fallback for operands outside the exact fast paths. */
@@ -572,6 +578,9 @@ struct Sph
 {
     static constexpr int LO = PRIM, HI = PRIM + 1;
     static constexpr bool UNION_ONLY = true; /* no Intersection / Difference at or below */
+    static constexpr bool NO_DIFF = true; /* no Difference at or below */
+    template <class PS>
+    __device__ static __forceinline__ int isect_empty(const PS &) { return 1; }
     struct Ctx
     {
         V3 omc;
@@ -723,6 +732,9 @@ struct Pln
 {
     static constexpr int LO = PRIM, HI = PRIM + 1;
     static constexpr bool UNION_ONLY = true; /* no Intersection / Difference at or below */
+    static constexpr bool NO_DIFF = true; /* no Difference at or below */
+    template <class PS>
+    __device__ static __forceinline__ int isect_empty(const PS &) { return 1; }
     struct Ctx
     {
         float num;
@@ -926,7 +938,20 @@ struct Pln
 
 /* Each merge step decides what to emit and which child to advance, then
  * advances each child at exactly ONE call site: the inlined code of a CSG
- * tree stays linear in its node count instead of multiplying per level. */
+ * tree stays linear in its node count instead of multiplying per level.
+ * PT_PULL_SELECT: the step's span copies as value selects.  The branchy form
+ * copies spans through a pointer the branch picks (out = s.sa / s.sb), which
+ * keeps the whole iterator state in private memory (scratch); the select form
+ * keeps it in registers.  That pays where the lazy merge is on the hot path
+ * (lane walks: C5's private segment 776 -> 100 B) and costs registers where it
+ * is rare (burst slow passes). */
+#ifndef PT_PULL_SELECT
+#if defined(PT_LANE_WALK)
+#define PT_PULL_SELECT 1
+#else
+#define PT_PULL_SELECT 0
+#endif
+#endif
 
 /* src/union.cpp:84-134 */
 template <class A, class B>
@@ -934,6 +959,9 @@ struct Uni
 {
     static constexpr int KIND = NODE_UNION;
     static constexpr bool UNION_ONLY = A::UNION_ONLY && B::UNION_ONLY;
+    static constexpr bool NO_DIFF = A::NO_DIFF && B::NO_DIFF;
+    template <class PS>
+    __device__ static __forceinline__ int isect_empty(const PS &ps) { return A::isect_empty(ps) & B::isect_empty(ps); }
     PTD_BINARY_COMMON
     template <class SEL>
     __device__ static constexpr bool clear_ok() { return A::template clear_ok<SEL>() && B::template clear_ok<SEL>(); }
@@ -943,6 +971,38 @@ struct Uni
         A::each_pos(f);
         B::each_pos(f);
     }
+#if PT_PULL_SELECT
+    __device__ static __forceinline__ bool pull(St &s, CS &out)
+    {
+        for (;;) {
+            if (s.ea && s.eb)
+                return false;
+            /* the step's decisions as values: the span copies are selects,
+             * never a copy through a pointer chosen by the branch (which
+             * keeps the iterator state out of registers) */
+            const bool ea = s.ea, eb = s.eb, both = !ea && !eb;
+            const float a0 = s.sa.t0, a1 = s.sa.t1, b0 = s.sb.t0, b1 = s.sb.t1;
+            const u32 ra0 = s.sa.r0, ra1 = s.sa.r1, rb0 = s.sb.r0, rb1 = s.sb.r1;
+            const bool sepA = both && a1 < b0, sepB = both && !(a1 < b0) && b1 < a0;
+            const bool over = both && !(a1 < b0) && !(b1 < a0);
+            const bool aFirst = over && a0 < b0, bFirst = over && !(a0 < b0);
+            const bool takeA = (!ea && eb) || sepA;
+            const bool emit = ea || takeA || sepB;
+            const bool adv_a = takeA || bFirst;
+            out.t0 = takeA ? a0 : b0, out.t1 = takeA ? a1 : b1;
+            out.r0 = takeA ? ra0 : rb0, out.r1 = takeA ? ra1 : rb1;
+            const bool extA = aFirst && a1 < b1, extB = bFirst && a1 > b1; /* end_from_end */
+            s.sa.t1 = extA ? b1 : a1, s.sa.r1 = extA ? rb1 : ra1;
+            s.sb.t1 = extB ? a1 : b1, s.sb.r1 = extB ? ra1 : rb1;
+            if (adv_a)
+                s.ea = !A::pull(s.a, s.sa);
+            else
+                s.eb = !B::pull(s.b, s.sb);
+            if (emit)
+                return true;
+        }
+    }
+#else
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
         for (;;) {
@@ -974,6 +1034,7 @@ struct Uni
                 return true;
         }
     }
+#endif
 };
 
 /* src/intersection.cpp:84-130 */
@@ -982,11 +1043,52 @@ struct Isect
 {
     static constexpr int KIND = NODE_ISECT;
     static constexpr bool UNION_ONLY = false;
+    static constexpr bool NO_DIFF = A::NO_DIFF && B::NO_DIFF;
+    /* the intersection is empty, or ends before EPS, when every primitive
+     * span below A is strictly separated from every one below B or one of
+     * the two ends before EPS (with no Difference below, A's and B's output
+     * spans lie inside the union of their primitives' spans) */
+    template <class PS>
+    __device__ static __forceinline__ int isect_empty(const PS &ps)
+    {
+        int ok = A::isect_empty(ps) & B::isect_empty(ps);
+        A::template each_sel<AllPrims>([&](auto x, auto) {
+            B::template each_sel<AllPrims>([&](auto y, auto) {
+                constexpr int X = decltype(x)::value, Y = decltype(y)::value;
+                ok &= sep(ps, X, Y) | inert(ps, X) | inert(ps, Y);
+            });
+        });
+        return ok;
+    }
     PTD_BINARY_COMMON
     template <class SEL>
     __device__ static constexpr bool clear_ok() { return A::template nsel<SEL>() + B::template nsel<SEL>() == 0; }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&) {}
+#if PT_PULL_SELECT
+    __device__ static __forceinline__ bool pull(St &s, CS &out)
+    {
+        for (;;) {
+            if (s.ea || s.eb)
+                return false;
+            const float a0 = s.sa.t0, a1 = s.sa.t1, b0 = s.sb.t0, b1 = s.sb.t1;
+            const bool skipA = a1 < b0, skipB = !skipA && b1 < a0, over = !skipA && !skipB;
+            /* overlap: the later start (start_from_start) and the earlier end;
+             * the span whose end is taken is advanced */
+            const bool bLater = over && a0 < b0;
+            const bool endA = over && (bLater ? a1 < b1 : !(b1 < a1));
+            out.t0 = bLater ? b0 : a0, out.r0 = bLater ? s.sb.r0 : s.sa.r0;
+            out.t1 = endA ? a1 : b1, out.r1 = endA ? s.sa.r1 : s.sb.r1;
+            const bool adv_a = skipA || endA;
+            if (adv_a)
+                s.ea = !A::pull(s.a, s.sa);
+            else
+                s.eb = !B::pull(s.b, s.sb);
+            if (over)
+                return true;
+        }
+    }
+#else
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
         for (;;) {
@@ -1018,6 +1120,7 @@ struct Isect
                 return true;
         }
     }
+#endif
 };
 
 /* src/difference.cpp:84-135, including the :124-130 copyEndFromStart quirk */
@@ -1026,11 +1129,48 @@ struct Diff
 {
     static constexpr int KIND = NODE_DIFF;
     static constexpr bool UNION_ONLY = false;
+    static constexpr bool NO_DIFF = false;
+    template <class PS>
+    __device__ static __forceinline__ int isect_empty(const PS &) { return 0; }
     PTD_BINARY_COMMON
     template <class SEL>
     __device__ static constexpr bool clear_ok() { return A::template nsel<SEL>() + B::template nsel<SEL>() == 0; }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { A::each_pos(f); }
+#if PT_PULL_SELECT
+    __device__ static __forceinline__ bool pull(St &s, CS &out)
+    {
+        for (;;) {
+            if (s.ea)
+                return false;
+            const bool eb = s.eb;
+            const float a0 = s.sa.t0, a1 = s.sa.t1, b0 = s.sb.t0, b1 = s.sb.t1;
+            const u32 ra0 = s.sa.r0, ra1 = s.sa.r1, rb0 = s.sb.r0, rb1 = s.sb.r1;
+            const bool passA = eb || a1 < b0;                     /* A emitted whole           */
+            const bool skipB = !passA && b1 < a0;                 /* B before A: next B        */
+            const bool over = !passA && !skipB;
+            const bool cut = over && a0 < b0;                     /* A emitted up to B's start */
+            const bool cutEnd = cut && a1 < b1;                   /*   ... and A is done       */
+            const bool cutSplit = cut && !(a1 < b1);              /*   ... A resumes after B   */
+            const bool quirk = over && !cut && a1 > b1;           /* :124-130, copyEndFromStart */
+            const bool emit = passA || cut;
+            const bool adv_a = passA || cutEnd || (over && !cut && !quirk);
+            /* emitted span: A's start, and A's end or B's start (flipped) */
+            out.t0 = a0, out.r0 = ra0;
+            out.t1 = cut ? b0 : a1, out.r1 = cut ? rb0 ^ FLIP : ra1;
+            /* A's state when it stays: resumes at B's end (start_from_end), or
+             * the quirk's end from B's start (end_from_start) */
+            s.sa.t0 = cutSplit ? b1 : a0, s.sa.r0 = cutSplit ? rb1 ^ FLIP : ra0;
+            s.sa.t1 = quirk ? b0 : a1, s.sa.r1 = quirk ? rb0 ^ FLIP : ra1;
+            if (adv_a)
+                s.ea = !A::pull(s.a, s.sa);
+            else
+                s.eb = !B::pull(s.b, s.sb);
+            if (emit)
+                return true;
+        }
+    }
+#else
     __device__ static __forceinline__ bool pull(St &s, CS &out)
     {
         for (;;) {
@@ -1067,6 +1207,7 @@ struct Diff
                 return true;
         }
     }
+#endif
 };
 
 /* TransformedObject (include/object.h:26-76): the child sees the ray mapped by
@@ -1077,6 +1218,9 @@ struct Xf
 {
     static constexpr int LO = C::LO, HI = C::HI;
     static constexpr bool UNION_ONLY = C::UNION_ONLY; /* spans keep the ray's t */
+    static constexpr bool NO_DIFF = C::NO_DIFF;
+    template <class PS>
+    __device__ static __forceinline__ int isect_empty(const PS &ps) { return C::isect_empty(ps); }
     struct Ctx
     {
         typename C::Ctx c;
@@ -1163,13 +1307,21 @@ __device__ __forceinline__ bool first_hit(const typename R::Ctx &ctx, V3 d, cons
  * chosen primitive.  Returns the check's verdict; the result is valid only
  * where it holds. */
 template <class R, class PS>
+__device__ __forceinline__ int cheap_ok(const PS &ps);
+template <class R, class PS>
 __device__ __forceinline__ int span_first_hit(const PS &ps, bool &hit, float &t, u32 &ref, bool &exit_hit)
 {
     int fok;
-    if constexpr (R::UNION_ONLY)
-        fok = union_min_ok(ps, [&](auto &&f) { R::each_pos(f); }) || R::fast_ok(ps);
-    else
+    if constexpr (R::NO_DIFF) {
+        /* one pass over the spans; the pairwise checks only where it cannot decide */
+        fok = cheap_ok<R>(ps);
+        if (wave_any(!fok)) {
+            if (!fok)
+                fok = R::fast_ok(ps);
+        }
+    } else {
         fok = R::fast_ok(ps);
+    }
     int found = 0;
     u32 bref = 0u;
     float b0 = 0.0f, b1 = 0.0f;
@@ -1283,6 +1435,21 @@ __device__ __forceinline__ int union_min_ok(const PS &ps, EACH &&each)
         found |= cand;
     });
     return ((!found) | ((b0 >= EPS) & !tie)) & !bad;
+}
+
+/* The one-pass check of a tree without Difference nodes: its Intersections
+ * are empty or end before EPS (isect_empty), so only Unions and transforms
+ * combine what can be met at or after EPS -- the union rule over the
+ * positive primitives (each_pos leaves Intersection subtrees out). */
+template <class R, class PS>
+__device__ __forceinline__ int cheap_ok(const PS &ps)
+{
+    static_assert(R::NO_DIFF, "cheap_ok needs a tree without Difference nodes");
+    const int u = union_min_ok(ps, [&](auto &&f) { R::each_pos(f); });
+    if constexpr (R::UNION_ONLY)
+        return u;
+    else
+        return u & R::isect_empty(ps);
 }
 
 /* ---- clear pass -------------------------------------
@@ -1760,6 +1927,7 @@ struct Counters
     u64 queries, leaf, attempts, rounds, shaded, nonleaf, slow, dark, mid;
 #ifdef PT_PHASE_TIMING
     u64 ph[7]; /* cycles: generation, its attempts, fast pass, slow pass, accumulation, burst total, sample total */
+    u64 ch[3]; /* cycles of the chunk loop: all of it, the lane-parallel front end, the result writes */
     u64 sp[2]; /* cycles of the spine: its span queries, the rest of its node work outside bursts */
     u64 np[8]; /* events: bursts, loop iterations, (unused), fast passes, slow passes, accumulations, fast lanes, slow lanes */
 #define PT_CNT(c, k, v) (c).np[k] += (v)
@@ -1777,7 +1945,9 @@ struct Counters
 #ifdef PT_PHASE_TIMING
 #define PT_T0(v) const u64 v = __builtin_amdgcn_s_memtime()
 #define PT_ACC(c, k, v) (c).ph[k] += __builtin_amdgcn_s_memtime() - (v)
+#define PT_ACC2(c, k, v) (c).ch[k] += __builtin_amdgcn_s_memtime() - (v)
 #else
+#define PT_ACC2(c, k, v)
 #define PT_T0(v)
 #define PT_ACC(c, k, v)
 #endif
@@ -1848,6 +2018,13 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 #define PT_LANE_MAJOR 1 /* deferred rounds: lane l evaluates attempts 8l..8l+7 (one chained stream) */
 #endif
 
+#ifndef PT_PASS_PAIR_FALLBACK
+/* 0: in a burst's fast pass over a Difference-free tree, lanes the one-pass
+ * check cannot decide go to the full merge directly instead of through the
+ * pairwise checks (whose all-pairs code raises the pass's register pressure
+ * for lanes that are rare there) */
+#define PT_PASS_PAIR_FALLBACK 0
+#endif
 /* Per-wave LDS work areas of the scatter loop. */
 struct WaveLds
 {
@@ -2272,10 +2449,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     slot = mbcnt(K[k], slot);
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k++) {
-                    if (in_mask(K[k] & __ballot(slot < slot_end)))
-                        ring[slot & (PT_RCAP - 1)] = make_float4(__uint_as_float((u32)s_lane),
-                                                                 __uint_as_float((u32)(s_lane >> 32)),
-                                                                 __int_as_float(k), 0.0f);
+                    if (in_mask(K[k] & __ballot(slot < slot_end))) {
+                        /* two stores, not one 16-byte one: a float4 of (state, k)
+                         * would be one more 4-register value live across the loop */
+                        float4 *r = &ring[slot & (PT_RCAP - 1)];
+                        __builtin_memcpy(r, &s_lane, 8);
+                        r->z = __int_as_float(k);
+                    }
                     slot = add_lane_bit(slot, K[k]);
                 }
                 /* failures after the round's last accepted attempt (lane L,
@@ -2449,14 +2629,17 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             S::Root::span(ps, ctx, mkray(dir), e);
             PT_MARK(10);
             int fok;
-            if constexpr (S::Root::UNION_ONLY) {
-                /* the union rule over every primitive; the pairwise checks
-                 * only where it cannot decide */
-                fok = union_min_ok(ps, [&](auto &&f) { S::Root::each_pos(f); });
+            if constexpr (S::Root::NO_DIFF) {
+                /* the union rule over the positive primitives (and empty
+                 * intersections); the pairwise checks only where it cannot
+                 * decide */
+                fok = cheap_ok<typename S::Root>(ps);
+#if PT_PASS_PAIR_FALLBACK
                 if (wave_any(!fok)) {
                     if (!fok)
                         fok = S::Root::fast_ok(ps);
                 }
+#endif
             } else {
                 fok = S::Root::fast_ok(ps);
             }
@@ -3451,7 +3634,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     /* engine jumps of 3l and 24l draws (A, G * inc): JumpLds */
     __shared__ u64 jbuf[64][2];
     __shared__ u64 jbuf24[64][2];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    /* the wave index as a scalar: the LDS bases derived from it stay in SGPRs */
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const u64 t_start = __builtin_amdgcn_s_memrealtime(); /* 100 MHz: wave lifetimes, stats[26..29] */
     const Env e = {P, imgs};
 #ifdef PT_POISON_LDS
@@ -3486,6 +3670,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
     cnt.sp[0] = cnt.sp[1] = 0;
+    cnt.ch[0] = cnt.ch[1] = cnt.ch[2] = 0;
 #endif
     const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
@@ -3511,6 +3696,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         next = dequeue();
 #endif
         const long long item0 = chunk * CH;
+        PT_T0(tchunk);
         /* the chunk's camera queries, one per lane */
         CamHit ch = {0, 0.0f, 0u, 0};
         int ldone = 0, lq = 0, lsh = 0;
@@ -3540,6 +3726,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             ldone = lane_sample<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
 #endif
         }
+        PT_ACC2(cnt, 1, tchunk); /* the lane-parallel front end */
         {
             /* statistics of the samples finished by their lane */
 #if defined(PT_LANE_WALK) || defined(PT_LANE_SCATTER)
@@ -3580,6 +3767,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         }
         const uint4 mr = lb[lane];
         const V3 mine = mk(__uint_as_float(mr.x), __uint_as_float(mr.y), __uint_as_float(mr.z));
+        PT_T0(tout);
 #if !PT_DEQUEUE_PREFETCH
         next = dequeue();
 #endif
@@ -3615,6 +3803,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             out[3 * st + 1] = mine.y;
             out[3 * st + 2] = mine.z;
         }
+        PT_ACC2(cnt, 2, tout);
+        PT_ACC2(cnt, 0, tchunk);
     }
     if (lane == 0) {
         atomicAdd(&stats[0], cnt.queries);
@@ -3637,6 +3827,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         for (int k = 0; k < 8; k++)
             atomicAdd(&stats[16 + k], cnt.np[k]);
         atomicAdd(&stats[30], cnt.sp[0]);
+        atomicAdd(&stats[25], cnt.ch[0]);
+        atomicAdd(&stats[32], cnt.ch[1]);
+        atomicAdd(&stats[33], cnt.ch[2]);
         atomicAdd(&stats[31], cnt.sp[1]);
 #endif
     }

@@ -443,7 +443,7 @@ DeviceState &device_state(SceneImpl &s, int device, const Generated &g)
         std::vector<uint64_t> jt = jump_table();
         ds->jump.ensure(jt.size());
         HIPCHECK(hipMemcpy(ds->jump.p, jt.data(), jt.size() * 8, hipMemcpyHostToDevice));
-        ds->stats.ensure(32);
+        ds->stats.ensure(40);
     }
     if (ds->key != g.key) {
         const std::vector<char> &code = code_object(g);
@@ -650,7 +650,7 @@ void collect_timings(DeviceState &ds, pt_render_stats *st)
         }
         st->samples += pr.samples;
     }
-    uint64_t c[32];
+    uint64_t c[40];
     HIPCHECK(hipMemcpy(c, ds.stats.p, sizeof c, hipMemcpyDeviceToHost));
     st->queries = c[0] + c[1];
     st->leaf_queries = c[1];
@@ -670,6 +670,7 @@ void collect_timings(DeviceState &ds, pt_render_stats *st)
             fprintf(stderr, " %llu", (unsigned long long)c[k]);
         fprintf(stderr, " %llu", (unsigned long long)c[25]); /* whole chunk loop */
         fprintf(stderr, " %llu %llu", (unsigned long long)c[30], (unsigned long long)c[31]); /* spine queries */
+        fprintf(stderr, " %llu %llu", (unsigned long long)c[32], (unsigned long long)c[33]); /* lane front end, writes */
         fprintf(stderr, "\n");
     }
     st->sphere_tests = st->queries * (uint64_t)ds.pending.back().n_spheres;
@@ -704,7 +705,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
     const bool timed = tm != Timing::None;
     /* the counters restart with the first recorded render */
     if (!timed || ds.pending.empty())
-        HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 32 * 8, stream));
+        HIPCHECK(hipMemsetAsync(ds.stats.p, 0, 40 * 8, stream));
     hipFunction_t fn = p->order == PT_ORDER_REFERENCE ? ds.strict : ds.fast;
     PendingRender pr;
     pr.n_spheres = g.n_spheres, pr.n_planes = g.n_planes;
