@@ -2014,6 +2014,17 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
     for (int i = 0; i < LdsBox<T>::N; i++)
         b.w[i] = u.w[i];
 }
+/* The wave index as a scalar (readfirstlane) or a vector value: a register
+ * allocation choice with opposite effects per scene class (same-box A/B,
+ * profiles/round4/ab_wave_index_ring_split.txt): Difference-free trees
+ * (C2) +4.5 %, trees with a Difference (C3) -3.5 %, C5 +-0.  -1 = by scene. */
+#ifndef PT_SCALAR_WAVE
+#define PT_SCALAR_WAVE -1
+#endif
+/* lane-major ring entries as two stores (C2 +8 %, C3 and C5 +-0, same A/B) */
+#ifndef PT_RING_SPLIT
+#define PT_RING_SPLIT 1
+#endif
 #ifndef PT_LANE_MAJOR
 #define PT_LANE_MAJOR 1 /* deferred rounds: lane l evaluates attempts 8l..8l+7 (one chained stream) */
 #endif
@@ -2452,9 +2463,15 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     if (in_mask(K[k] & __ballot(slot < slot_end))) {
                         /* two stores, not one 16-byte one: a float4 of (state, k)
                          * would be one more 4-register value live across the loop */
+#if PT_RING_SPLIT
                         float4 *r = &ring[slot & (PT_RCAP - 1)];
                         __builtin_memcpy(r, &s_lane, 8);
                         r->z = __int_as_float(k);
+#else
+                        ring[slot & (PT_RCAP - 1)] = make_float4(__uint_as_float((u32)s_lane),
+                                                                 __uint_as_float((u32)(s_lane >> 32)),
+                                                                 __int_as_float(k), 0.0f);
+#endif
                     }
                     slot = add_lane_bit(slot, K[k]);
                 }
@@ -3634,8 +3651,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     /* engine jumps of 3l and 24l draws (A, G * inc): JumpLds */
     __shared__ u64 jbuf[64][2];
     __shared__ u64 jbuf24[64][2];
-    /* the wave index as a scalar: the LDS bases derived from it stay in SGPRs */
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    constexpr bool SCALAR_WAVE = PT_SCALAR_WAVE < 0 ? S::Root::NO_DIFF : PT_SCALAR_WAVE != 0;
+    const int wave = SCALAR_WAVE ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
     const u64 t_start = __builtin_amdgcn_s_memrealtime(); /* 100 MHz: wave lifetimes, stats[26..29] */
     const Env e = {P, imgs};
 #ifdef PT_POISON_LDS

@@ -206,8 +206,10 @@ CONFIGS: Dict[str, Config] = {
     "C1": Config("C1", 256, 256, 16, 4, scene_p0, note="plumbing; CPU reference path"),
     # C2 without matBrightDiffuseWhite: with it the reference's own cost per
     # sample has no practical bound (C2_FULL below)
+    # C2 with span-first spine queries since round 4 (same box, 65 536 hashed
+    # pixels at 16 spp: 4.83 -> 4.91 Msamples/s)
     "C2": Config("C2", 1280, 720, 256, 16, lambda procedural=False: scene_c2(procedural, full_mix=False),
-                 note="8 spheres (no matBrightDiffuseWhite) + plane + mirror-ball env (test2.hdr)"),
+                 note="8 spheres (no matBrightDiffuseWhite) + plane + mirror-ball env (test2.hdr)", fast_spine=True),
     # C3/C4: span-first spine queries (same-box A/B at 1024 spp: 156.3 -> 157.2
     # Msamples/s; round 2's kernel lost 0.9 % with them)
     "C3": Config("C3", 1920, 1080, 1024, 8, scene_p1, note="north star: 6-sphere union/difference CSG",

@@ -22,7 +22,10 @@ print("compile %.1fs" % (time.time() - t))
 cache = os.path.join(ROOT, "path-trace_amd", "_jit_cache")
 hsaco = [os.path.join(cache, f) for f in os.listdir(cache) if f.endswith(".hsaco")]
 hsaco.sort(key=os.path.getmtime)
-f = hsaco[-1]
+f = os.path.join(cache, key + ".hsaco")
+if not os.path.exists(f):
+    f = hsaco[-1]
+print("code object", os.path.basename(f))
 notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", f], capture_output=True, text=True).stdout
 for line in notes.splitlines():
     if any(k in line for k in (".name:", "vgpr_count", "sgpr_count", "spill", "private_segment_fixed_size",

@@ -29,4 +29,10 @@ print(json.dumps({"config": name, "spp": spp, "adaptive_wall_s": ta, "adaptive_k
                   "levels": info["levels"], "lookahead_pixels": info["lookahead_pixels"],
                   "exact_batches": {"wall_s": tx, "kernel_ms": info_x["kernel_ms"], "levels": info_x["levels"]},
                   "full_wall_s": tf, "full_kernel_ms": st["kernel_ms"],
+                  # the work the adaptive batches did (traced + lookahead points) against the frame's:
+                  # time at the frame's rate for that work = full_kernel_ms * query_frac
+                  "adaptive_samples": info["samples"], "adaptive_queries": info["queries"],
+                  "full_samples": st["samples"], "full_queries": st["queries"],
+                  "sample_frac": info["samples"] / st["samples"], "query_frac": info["queries"] / st["queries"],
+                  "ms_at_frame_rate": st["kernel_ms"] * info["queries"] / st["queries"],
                   "rmse_adaptive_vs_full": rmse}), flush=True)
