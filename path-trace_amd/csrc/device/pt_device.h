@@ -573,6 +573,9 @@ struct AllPrims
 /* Sphere (src/sphere.cpp:31-49).  P[OFF..OFF+3] = center, r*r.  Branch-free:
  * t0/t1 are computed on every lane (dead lanes' values are never read), with
  * one wave-uniform fallback for operands outside the exact fast paths. */
+#ifndef PT_SPHERE_SKIP
+#define PT_SPHERE_SKIP 0
+#endif
 template <int PRIM, int OFF, int MAT>
 struct Sph
 {
@@ -623,6 +626,15 @@ struct Sph
         const float b = dot(c.omc, q.d);
         const float disc = b * b - q.a * c.c;
         const bool live = !(disc <= EPS);
+#if PT_SPHERE_SKIP
+        /* no lane meets the sphere: skip the root and the divisions (a dead
+         * span's bounds are never read) */
+        if (!wave_any(live)) {
+            s.live = 0;
+            s.t0 = s.t1 = __builtin_nanf("");
+            return;
+        }
+#endif
         const float sq = sqrt_core(disc); /* exact: disc > EPS (or inf/NaN) where live */
         const float n0 = -b - sq, n1 = -b + sq;
         float t0 = div_core(n0, q.ra), t1 = div_core(n1, q.ra);
