@@ -249,6 +249,11 @@ Generated generate(const SceneImpl &s, int depth)
     /* per-scene lane walk with scatter loops (pt_scene_set_lane_scatter) */
     if (s.lane_scatter)
         src << "#define PT_LANE_SCATTER 1\n";
+    /* Difference-free trees skip a sphere's root and divisions when no lane of
+     * the wave meets it (pt_device.h PT_SPHERE_SKIP; same-box A/B,
+     * profiles/round4/ab_sphere_skip.txt: C2 +7.2 %, C5 +0.3 %, C3 -10 %) */
+    if (root.find("Diff<") == std::string::npos)
+        src << "#ifndef PT_SPHERE_SKIP\n#define PT_SPHERE_SKIP 1\n#endif\n";
     /* experiment hook: A/B a different device library text in the same run,
      * e.g. PT_DEVICE_HEADER=tools/ab/old.h (profiling only) */
     if (const char *hdr = getenv("PT_DEVICE_HEADER")) {
