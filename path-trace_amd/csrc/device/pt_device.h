@@ -366,6 +366,15 @@ __device__ __forceinline__ int mbcnt(u64 m, int base)
 {
     return (int)__builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, (u32)base));
 }
+/* The lane index recomputed where it is used (v_mbcnt of all ones): an asm
+ * the compiler can neither merge nor hoist, so no register holds it across a
+ * burst -- where it was spilled to scratch in scenes under VGPR pressure. */
+__device__ __forceinline__ int lane_id()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 /* this lane's bit of the uniform mask m, by arithmetic */
 __device__ __forceinline__ bool lane_in(u64 m) { return (m >> (threadIdx.x & 63)) & 1ull; }
 /* the same as a branch condition: `if (in_mask(m))` runs the block with exec = m
@@ -2034,6 +2043,15 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 #define PT_SCALAR_WAVE -1
 #endif
 /* lane-major ring entries as two stores (C2 +8 %, C3 and C5 +-0, same A/B) */
+/* lane index recomputed at each use in bursts (lane_id); 0 = held in a register */
+#ifndef PT_LANE_REMAT
+#define PT_LANE_REMAT 0
+#endif
+/* the fast order's lane sums in LDS instead of registers: -1 = where the
+ * 768 B per wave leave the workgroups per CU unchanged (min_workgroups) */
+#ifndef PT_LSUM_LDS
+#define PT_LSUM_LDS 0
+#endif
 #ifndef PT_RING_SPLIT
 #define PT_RING_SPLIT 1
 #endif
@@ -2055,6 +2073,7 @@ struct WaveLds
     float4 *ring;         /* PT_RCAP kept-child slots: parked ray, then the child's term */
     unsigned char *slowq; /* PT_SCAP slots waiting for the full merge (ring number mod 256) */
     unsigned char *midq;  /* PT_SCAP slots the clear pass could not finish (fast check next) */
+    float *lsum;          /* the fast order's 64 lane sums, x / y / z planes (lsum_lds scenes) */
 };
 
 /* ---------------------------------------------------------------- spine --- */
@@ -2307,8 +2326,12 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 {
     float4 *const ring = L.ring;
     unsigned char *const slowq = L.slowq, *const midq = L.midq;
+#if PT_LANE_REMAT
+#define lane lane_id()
+#else
     const int lane = threadIdx.x & 63;
-    const u64 below = (1ull << lane) - 1ull;
+#endif
+    const bool LSUM_LDS = L.lsum != nullptr; /* a constant: render_chunk sets it per scene */
     const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
     const float sc = unif(f.sc), strength = unif(f.strength), add = unif(f.add);
     const int depth = uni(f.depth), N = uni(f.N);
@@ -2352,6 +2375,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     int npos = 0, nkeep = 0, keep_sum = 0, nzc = 0, f_n = 0, s_head = 0, s_n = 0, s_first = 0;
     int m_head = 0, m_n = 0, m_first = 0;
     V3 lsum = mk(0.0f, 0.0f, 0.0f);
+    if (LSUM_LDS)
+        L.lsum[lane] = L.lsum[64 + lane] = L.lsum[128 + lane] = 0.0f;
     int fast_on = 1, clear_on = 1;
     /* the clear pass applies when every emissive primitive hangs off the root
      * through Unions and transforms only */
@@ -2690,7 +2715,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
          * queue of ring numbers. */
         auto enqueue = [&](unsigned char *q, int head, int &qn, int &qfirst, u64 SM, int pos0, int pos) {
             if ((SM >> lane) & 1ull)
-                q[(head + qn + __popcll(SM & below)) & (PT_SCAP - 1)] = (unsigned char)pos;
+                q[mbcnt(SM, head + qn) & (PT_SCAP - 1)] = (unsigned char)pos;
             if (qn == 0 && SM)
                 qfirst = pos0 + __builtin_ctzll(SM);
             qn += __popcll(SM);
@@ -2743,7 +2768,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 const u64 SM = __ballot(slow);
                 const int p0 = uni(__builtin_amdgcn_readlane(pos, SM ? __builtin_ctzll(SM) : 0));
                 if ((SM >> lane) & 1ull)
-                    slowq[(s_head + s_n + __popcll(SM & below)) & (PT_SCAP - 1)] = (unsigned char)pos;
+                    slowq[mbcnt(SM, s_head + s_n) & (PT_SCAP - 1)] = (unsigned char)pos;
                 if (s_n == 0 && SM)
                     s_first = p0;
                 s_n += __popcll(SM);
@@ -2878,7 +2903,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     t = mk(__int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(t.x))),
                            __int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(t.y))),
                            __int_as_float(__builtin_amdgcn_ds_permute(to, __float_as_int(t.z))));
-                    lsum = lsum + t;
+                    if (LSUM_LDS) {
+                        float *const q = L.lsum;
+                        const int l = lane;
+                        q[l] = q[l] + t.x, q[64 + l] = q[64 + l] + t.y, q[128 + l] = q[128 + l] + t.z;
+                    } else {
+                        lsum = lsum + t;
+                    }
                     nzc += pnz;
                 }
                 keep_sum += c;
@@ -2889,8 +2920,13 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             break;
     }
     /* the run's end: retval + the pairwise tree of the 64 lane sums */
-    if (!STRICT && npos > 0)
+    if (!STRICT && npos > 0) {
+        if (LSUM_LDS) {
+            const int l = lane;
+            lsum = mk(L.lsum[l], L.lsum[64 + l], L.lsum[128 + l]);
+        }
         retval = wave_tree_sum3_add(lsum, retval);
+    }
     /* leaf children of the burst (each one span query) and the dark ones among them */
     cadd(cnt.leaf, (u32)npos);
     cadd(cnt.dark, (u32)(npos - nkeep));
@@ -2898,6 +2934,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     f.i = i + npos;
     return reason;
 }
+#if PT_LANE_REMAT
+#undef lane
+#endif
 
 /* Every child is provably a leaf when depth-1 <= 0 or when even the largest
  * possible factor (1 + 4e-7: wn and n are unit vectors) keeps the child
@@ -3637,6 +3676,34 @@ __device__ __forceinline__ void item_slot(const PtLaunch &lp, long long item, lo
 #define PT_DEQUEUE_PREFETCH 0 /* same-box A/B: C3 -2 %, C5 +-0.5 % (the atomic's wait joins the chunk's first load) */
 #endif
 
+/* Workgroups per CU for the launch bounds: 5 (5 waves/SIMD, VGPRs capped at
+ * 96; A/B on C3: 4 -> 5 +6.6 %, 3 -> -13 %) when that many workgroups' LDS
+ * fits the CU's 160 KB, else as many as fit -- the frame stack grows with
+ * MAXD (depth 16: 4, depth 64: 2), and a cap whose extra wave cannot be
+ * resident would only spill registers. */
+template <class S, int MAXD, bool LSUM>
+__device__ constexpr int lds_workgroups()
+{
+    constexpr int lds = PT_WPW * ((MAXD + 1) * (int)sizeof(Frame) + 16 * PT_RCAP + 2 * PT_SCAP +
+                                  (int)sizeof(Counters) + (int)sizeof(LdsBox<typename S::Root::Ctx>) + 64 * 16 +
+                                  (LSUM ? 3 * 64 * 4 : 4)) +
+                        2 * 64 * 16;
+    constexpr int alloc = (lds + 1279) / 1280 * 1280; /* gfx950 LDS allocation unit (measured) */
+    constexpr int n = 160 * 1024 / alloc;
+    return n < 1 ? 1 : n > 5 ? 5 : n;
+}
+/* lane sums in LDS (PT_LSUM_LDS): forced, or where they cost no workgroup per CU */
+template <class S, int MAXD>
+__device__ constexpr bool lsum_lds()
+{
+    return PT_LSUM_LDS < 0 ? lds_workgroups<S, MAXD, true>() == lds_workgroups<S, MAXD, false>() : PT_LSUM_LDS != 0;
+}
+template <class S, int MAXD>
+__device__ constexpr int min_workgroups()
+{
+    return lds_workgroups<S, MAXD, lsum_lds<S, MAXD>()>();
+}
+
 /* The megakernel body.  Persistent: the grid is sized to the resident
  * capacity and every wave pulls 64-item chunks from a global counter until
  * none are left.  Per-chunk cost varies by ~10^5 (sky pixels vs diffuse
@@ -3654,6 +3721,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     __shared__ unsigned char sbuf[PT_WPW][PT_SCAP];
     __shared__ unsigned char mbuf[PT_WPW][PT_SCAP];
     __shared__ Counters cbuf[PT_WPW];
+    constexpr bool LSUM_LDS = lsum_lds<S, MAXD>();
+    __shared__ float lsbuf[PT_WPW][LSUM_LDS ? 3 * 64 : 1];
     /* a chunk's lanes while the wave walks its samples one by one: (pixel,
      * sample | hit << 30 | exit << 31, camera t, camera ref), replaced by the
      * sample's result (x, y, z) once it is traced; in LDS rather than in
@@ -3702,7 +3771,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     cnt.sp[0] = cnt.sp[1] = 0;
     cnt.ch[0] = cnt.ch[1] = cnt.ch[2] = 0;
 #endif
-    const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave]};
+    const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave], LSUM_LDS ? lsbuf[wave] : nullptr};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
@@ -3865,21 +3934,6 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     }
 }
 
-/* Workgroups per CU for the launch bounds: 5 (5 waves/SIMD, VGPRs capped at
- * 96; A/B on C3: 4 -> 5 +6.6 %, 3 -> -13 %) when that many workgroups' LDS
- * fits the CU's 160 KB, else as many as fit -- the frame stack grows with
- * MAXD (depth 16: 4, depth 64: 2), and a cap whose extra wave cannot be
- * resident would only spill registers. */
-template <class S, int MAXD>
-__device__ constexpr int min_workgroups()
-{
-    constexpr int lds = PT_WPW * ((MAXD + 1) * (int)sizeof(Frame) + 16 * PT_RCAP + 2 * PT_SCAP +
-                                  (int)sizeof(Counters) + (int)sizeof(LdsBox<typename S::Root::Ctx>) + 64 * 16) +
-                        2 * 64 * 16;
-    constexpr int alloc = (lds + 1279) / 1280 * 1280; /* gfx950 LDS allocation unit (measured) */
-    constexpr int n = 160 * 1024 / alloc;
-    return n < 1 ? 1 : n > 5 ? 5 : n;
-}
 
 /* ---- boundary queries (pt_query_spans, pt_tex_eval) -------------------
  * The reference's query virtuals served on the device, one ray / point per
