@@ -358,7 +358,10 @@ public:
     /* getColor / getFloat (texture.h:13-18).  The built-in classes answer on
      * the device (pt_tex_eval of this texture, flattened once); a user-defined
      * subclass overrides getColor as in the reference -- it then works on the
-     * host, but has no device form, so a scene using it cannot be rendered. */
+     * host, but has no device form, so a scene using it cannot be rendered.
+     * The built-in classes are final and their fields const (Image is
+     * immutable too), so the flattened form cached on first use never goes
+     * stale and no override can be bypassed by the device path. */
     virtual Color getColor(Vector3D pos) const
     {
         Color c;
@@ -406,10 +409,10 @@ private:
     }
 };
 
-class ColorTexture : public Texture /* texture.h:29-58 */
+class ColorTexture final : public Texture /* texture.h:29-58 */
 {
 public:
-    Color color;
+    const Color color;
     ColorTexture(Color color) : Texture(true), color(color) {}
     ColorTexture(float r, float g, float b) : Texture(true), color(r, g, b) {}
     ColorTexture(float v) : Texture(true), color(v) {}
@@ -418,7 +421,7 @@ public:
     pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_color(f.s, color.x, color.y, color.z)); }
 };
 
-class TransformedTexture : public Texture /* texture.h:60-90 */
+class TransformedTexture final : public Texture /* texture.h:60-90 */
 {
 public:
     TransformedTexture(const Matrix &m, Texture *t) : Texture(true), m(m), t(t) {}
@@ -443,25 +446,25 @@ inline Texture *transform(const Matrix &m, Texture *t) /* texture.h:92-98 */
     return r ? r : new TransformedTexture(m, t->duplicate());
 }
 
-class ImageTexture : public Texture /* image_texture.h:9-33 */
+class ImageTexture final : public Texture /* image_texture.h:9-33 */
 {
 public:
     explicit ImageTexture(Image image) : Texture(true), image(image) {}
     Texture *duplicate() const override { return new ImageTexture(image); }
     pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_image(f.s, f.image(image))); }
-    Image image;
+    const Image image;
 };
 
-class ImageAlphaTexture : public Texture /* image_texture.h:35-70 */
+class ImageAlphaTexture final : public Texture /* image_texture.h:35-70 */
 {
 public:
     explicit ImageAlphaTexture(Image image) : Texture(true), image(image) {}
     Texture *duplicate() const override { return new ImageAlphaTexture(image); }
     pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_image_alpha(f.s, f.image(image))); }
-    Image image;
+    const Image image;
 };
 
-class ImageSkyboxTexture : public Texture /* image_texture.h:72-115 */
+class ImageSkyboxTexture final : public Texture /* image_texture.h:72-115 */
 {
 public:
     ImageSkyboxTexture(Image top, Image bottom, Image left, Image right, Image front, Image back)
@@ -478,10 +481,10 @@ public:
         for (int i = 0; i < 6; i++) id[i] = f.image(faces[i]);
         return ptCheck(pt_tex_skybox(f.s, id[0], id[1], id[2], id[3], id[4], id[5]));
     }
-    Image faces[6];
+    const Image faces[6];
 };
 
-class ImageSkyboxAlphaTexture : public Texture /* image_texture.h:117-181 */
+class ImageSkyboxAlphaTexture final : public Texture /* image_texture.h:117-181 */
 {
 public:
     ImageSkyboxAlphaTexture(Image top, Image bottom, Image left, Image right, Image front, Image back)
@@ -498,7 +501,7 @@ public:
         for (int i = 0; i < 6; i++) id[i] = f.image(faces[i]);
         return ptCheck(pt_tex_skybox_alpha(f.s, id[0], id[1], id[2], id[3], id[4], id[5]));
     }
-    Image faces[6];
+    const Image faces[6];
 };
 
 /* owning single-child wrappers: FilterTexture (filter_texture.h:8-28) and
@@ -513,7 +516,7 @@ protected:
     Texture *const t;
 };
 
-class MultiplyTexture : public WrapTexture /* filter_texture.h:30-48 */
+class MultiplyTexture final : public WrapTexture /* filter_texture.h:30-48 */
 {
 public:
     MultiplyTexture(Color factor, Texture *t) : WrapTexture(t), factor(factor) {}
@@ -522,10 +525,10 @@ public:
     {
         return ptCheck(pt_tex_multiply(f.s, factor.x, factor.y, factor.z, f.texture(t)));
     }
-    Color factor;
+    const Color factor;
 };
 
-class LogTexture : public WrapTexture /* filter_texture.h:50-80 */
+class LogTexture final : public WrapTexture /* filter_texture.h:50-80 */
 {
 public:
     explicit LogTexture(Texture *t) : WrapTexture(t) {}
@@ -533,7 +536,7 @@ public:
     pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_log(f.s, f.texture(t))); }
 };
 
-class MirrorBallSkymapTexture : public WrapTexture /* transform_texture.h:33-59 */
+class MirrorBallSkymapTexture final : public WrapTexture /* transform_texture.h:33-59 */
 {
 public:
     explicit MirrorBallSkymapTexture(Texture *t) : WrapTexture(t) {}
@@ -541,7 +544,7 @@ public:
     pt_id flatten(Flattener &f) const override { return ptCheck(pt_tex_mirrorball(f.s, f.texture(t))); }
 };
 
-class SphericalCoordinatesSkymapTexture : public WrapTexture /* :61-85 */
+class SphericalCoordinatesSkymapTexture final : public WrapTexture /* :61-85 */
 {
 public:
     explicit SphericalCoordinatesSkymapTexture(Texture *t) : WrapTexture(t) {}
