@@ -2043,12 +2043,15 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 #define PT_SCALAR_WAVE -1
 #endif
 /* lane-major ring entries as two stores (C2 +8 %, C3 and C5 +-0, same A/B) */
-/* lane index recomputed at each use in bursts (lane_id); 0 = held in a register */
+/* lane index recomputed at each use in bursts (lane_id) or held in a
+ * register; -1 = by scene: same-box A/B (profiles/round4/ab_lane_remat_lsum_lds.txt)
+ * Difference-free trees (C2) +6 %, C3 -1 %, C5 -0.1 % */
 #ifndef PT_LANE_REMAT
-#define PT_LANE_REMAT 0
+#define PT_LANE_REMAT -1
 #endif
 /* the fast order's lane sums in LDS instead of registers: -1 = where the
- * 768 B per wave leave the workgroups per CU unchanged (min_workgroups) */
+ * 768 B per wave leave the workgroups per CU unchanged (min_workgroups).
+ * Off: C2 +1..2.5 % alone, nothing on top of PT_LANE_REMAT; C3, C5 +-0 */
 #ifndef PT_LSUM_LDS
 #define PT_LSUM_LDS 0
 #endif
@@ -2326,11 +2329,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 {
     float4 *const ring = L.ring;
     unsigned char *const slowq = L.slowq, *const midq = L.midq;
-#if PT_LANE_REMAT
-#define lane lane_id()
-#else
-    const int lane = threadIdx.x & 63;
-#endif
+    constexpr bool LANE_REMAT = PT_LANE_REMAT < 0 ? S::Root::NO_DIFF : PT_LANE_REMAT != 0;
+    const int lane_reg = threadIdx.x & 63;
+#define lane (LANE_REMAT ? lane_id() : lane_reg)
     const bool LSUM_LDS = L.lsum != nullptr; /* a constant: render_chunk sets it per scene */
     const V3 hit = univ(f.hit), n = univ(f.n), rc = univ(f.rc);
     const float sc = unif(f.sc), strength = unif(f.strength), add = unif(f.add);
@@ -2934,9 +2935,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     f.i = i + npos;
     return reason;
 }
-#if PT_LANE_REMAT
 #undef lane
-#endif
 
 /* Every child is provably a leaf when depth-1 <= 0 or when even the largest
  * possible factor (1 + 4e-7: wn and n are unit vectors) keeps the child
