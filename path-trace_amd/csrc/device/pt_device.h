@@ -3671,8 +3671,16 @@ __device__ __forceinline__ void item_slot(const PtLaunch &lp, long long item, lo
 #ifndef PT_CHUNK
 #define PT_CHUNK 64 /* default (pixel, sample) items a wave takes per dequeue (<= 64) */
 #endif
+/* the next chunk's dequeue issued before this chunk's work (the atomic's wait
+ * joins the chunk's first load).  Same-box A/B, round 4
+ * (profiles/round4/ab_knobs_r4u.txt): C3 -0.5 %, C5 (lane walks) +0.36 %:
+ * on for lane-walk scenes */
 #ifndef PT_DEQUEUE_PREFETCH
-#define PT_DEQUEUE_PREFETCH 0 /* same-box A/B: C3 -2 %, C5 +-0.5 % (the atomic's wait joins the chunk's first load) */
+#if defined(PT_LANE_WALK)
+#define PT_DEQUEUE_PREFETCH 1
+#else
+#define PT_DEQUEUE_PREFETCH 0
+#endif
 #endif
 
 /* Workgroups per CU for the launch bounds: 5 (5 waves/SIMD, VGPRs capped at
