@@ -1369,14 +1369,16 @@ __device__ __forceinline__ int span_first_hit(const PS &ps, bool &hit, float &t,
  * the checks hold, else the lazy merge.  The checks are wave-uniform here. */
 template <class R>
 __device__ __forceinline__ bool spine_first_hit(const typename R::Ctx &ctx, V3 d, const Env &e, float &t, u32 &ref,
-                                                bool &exit_hit)
+                                                bool &exit_hit, int &merged)
 {
     PrimSpans<R::HI> ps;
     R::span(ps, ctx, mkray(d), e);
     bool hit;
     const int fok = span_first_hit<R>(ps, hit, t, ref, exit_hit);
+    merged = 0;
     if (!wave_any(!fok))
         return hit;
+    merged = 1;
     return first_hit<R>(ctx, d, e, t, ref, exit_hit);
 }
 
@@ -1949,7 +1951,7 @@ struct Counters
 #ifdef PT_PHASE_TIMING
     u64 ph[7]; /* cycles: generation, its attempts, fast pass, slow pass, accumulation, burst total, sample total */
     u64 ch[3]; /* cycles of the chunk loop: all of it, the lane-parallel front end, the result writes */
-    u64 sp[2]; /* cycles of the spine: its span queries, the rest of its node work outside bursts */
+    u64 sp[3]; /* the spine's span queries: cycles, count, those that ran the lazy merge */
     u64 np[8]; /* events: bursts, loop iterations, (unused), fast passes, slow passes, accumulations, fast lanes, slow lanes */
 #define PT_CNT(c, k, v) (c).np[k] += (v)
 #else
@@ -3513,7 +3515,11 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 typename S::Root::Ctx ctx;
                 S::Root::prep(ctx, o, e);
 #ifdef PT_FAST_SPINE /* per scene, pt_scene_set_fast_spine */
-                found = spine_first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+                int merged = 0;
+                found = spine_first_hit<typename S::Root>(ctx, d, e, t, ref, ex, merged);
+#ifdef PT_PHASE_TIMING
+                cnt.sp[2] += (u64)merged;
+#endif
 #else
                 found = first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
 #endif
@@ -3775,7 +3781,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         cnt.ph[k] = 0;
     for (int k = 0; k < 8; k++)
         cnt.np[k] = 0;
-    cnt.sp[0] = cnt.sp[1] = 0;
+    cnt.sp[0] = cnt.sp[1] = cnt.sp[2] = 0;
     cnt.ch[0] = cnt.ch[1] = cnt.ch[2] = 0;
 #endif
     const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave], LSUM_LDS ? lsbuf[wave] : nullptr};
@@ -3937,6 +3943,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         atomicAdd(&stats[32], cnt.ch[1]);
         atomicAdd(&stats[33], cnt.ch[2]);
         atomicAdd(&stats[31], cnt.sp[1]);
+        atomicAdd(&stats[34], cnt.sp[2]);
 #endif
     }
 }

@@ -671,6 +671,7 @@ void collect_timings(DeviceState &ds, pt_render_stats *st)
         fprintf(stderr, " %llu", (unsigned long long)c[25]); /* whole chunk loop */
         fprintf(stderr, " %llu %llu", (unsigned long long)c[30], (unsigned long long)c[31]); /* spine queries */
         fprintf(stderr, " %llu %llu", (unsigned long long)c[32], (unsigned long long)c[33]); /* lane front end, writes */
+        fprintf(stderr, " %llu", (unsigned long long)c[34]); /* spine queries that ran the lazy merge */
         fprintf(stderr, "\n");
     }
     st->sphere_tests = st->queries * (uint64_t)ds.pending.back().n_spheres;

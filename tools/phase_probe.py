@@ -40,6 +40,8 @@ for line in r.stderr.splitlines():
             print("%-12s %6.1f%%  result writes of the chunk loop" % ("writes", 100.0 * v[19] / v[15]))
         if len(v) >= 18 and v[17]:
             print("%-12s %6.1f%%  (%.0f cycles per query)" % ("spine-query", 100.0 * v[16] / tot, v[16] / v[17]))
+            if len(v) >= 21:
+                print("%-12s %6.1f%%  of the spine's queries ran the lazy merge" % ("spine-merge", 100.0 * v[20] / v[17]))
         if len(v) >= 15:
             import json as _j
             last = _j.loads(r.stdout.strip().splitlines()[-1])
