@@ -2024,6 +2024,25 @@ __device__ __forceinline__ T lds_get(const LdsBox<T> &b)
         u.w[i] = b.w[i];
     return u.t;
 }
+/* the same, each word kept a vector value (an empty asm on it): the
+ * compiler cannot turn the uniform words into SGPRs, which a scene under
+ * SGPR pressure spills into VGPR lanes and reads back one v_readlane at a time */
+template <class T>
+__device__ __forceinline__ T lds_get_v(const LdsBox<T> &b)
+{
+    union
+    {
+        float4 w[LdsBox<T>::N];
+        T t;
+    } u;
+#pragma unroll
+    for (int i = 0; i < LdsBox<T>::N; i++) {
+        float4 v = b.w[i];
+        asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+        u.w[i] = v;
+    }
+    return u.t;
+}
 template <class T>
 __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 {
@@ -2043,6 +2062,14 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
  * (C2) +4.5 %, trees with a Difference (C3) -3.5 %, C5 +-0.  -1 = by scene. */
 #ifndef PT_SCALAR_WAVE
 #define PT_SCALAR_WAVE -1
+#endif
+/* the pass queries' primitive contexts as vector values (lds_get_v) */
+#ifndef PT_CTX_VGPR
+#define PT_CTX_VGPR 0
+#endif
+/* the clear pass in union-only scenes too (round 2: off, C2 2.94 -> 3.37) */
+#ifndef PT_CLEAR_UNION
+#define PT_CLEAR_UNION 0
 #endif
 /* lane-major ring entries as two stores (C2 +8 %, C3 and C5 +-0, same A/B) */
 /* lane index recomputed at each use in bursts (lane_id) or held in a
@@ -2386,7 +2413,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     /* union-only scenes skip it: their first pass takes every primitive's
      * span and the union rule at once, which decides nearly every lane and
      * saves the mid queue's second pass (C2 2.94 -> 3.37 Msamples/s) */
-    constexpr bool CLEAR = S::Root::template clear_ok<Emissive<S>>() && !S::Root::UNION_ONLY;
+    constexpr bool CLEAR = S::Root::template clear_ok<Emissive<S>>() && (PT_CLEAR_UNION || !S::Root::UNION_ONLY);
     /* RAW: dark children are decided on the unnormalised direction (dark_mask,
      * sound but conservative).  The zero term also needs a factor >= +0, i.e.
      * a computed dot(normalize(w), n) >= 0: accepted w have a computed
@@ -2680,7 +2707,11 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
         auto fast_lane = [&](int pos, float4 en) -> bool {
             const V3 dir = mk(en.x, en.y, en.z);
             PT_MARK(8);
+#if PT_CTX_VGPR
+            const typename S::Root::Ctx ctx = lds_get_v(*cxp);
+#else
             const typename S::Root::Ctx ctx = lds_get(*cxp);
+#endif
             PrimSpans<S::Root::HI> ps;
             PT_MARK(9);
             S::Root::span(ps, ctx, mkray(dir), e);
