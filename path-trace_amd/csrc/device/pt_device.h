@@ -2063,7 +2063,8 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 #ifndef PT_SCALAR_WAVE
 #define PT_SCALAR_WAVE -1
 #endif
-/* the pass queries' primitive contexts as vector values (lds_get_v) */
+/* the pass queries' primitive contexts as vector values (lds_get_v); same-box
+ * A/B (profiles/round4/ab_ctx_vgpr.txt): C3 -0.8 %, C2 and C5 +-1 % -- off */
 #ifndef PT_CTX_VGPR
 #define PT_CTX_VGPR 0
 #endif
