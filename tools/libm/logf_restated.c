@@ -15,6 +15,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -66,10 +67,12 @@ static float my_logf(float x, int fused)
     return (float)y;
 }
 
-int main(void)
+int main(int argc, char **argv)
 {
+    /* optional stride: every k-th non-negative float (the test suite's quick form) */
+    const uint64_t step = argc > 1 ? strtoull(argv[1], NULL, 10) : 1;
     long bad[2] = {0, 0};
-    for (uint64_t u = 0; u < 0x80000000ull; u++) {
+    for (uint64_t u = 0; u < 0x80000000ull; u += step ? step : 1) {
         const float x = asf((uint32_t)u), g = logf(x);
         for (int f = 0; f < 2; f++) {
             const float m = my_logf(x, f);
@@ -80,7 +83,7 @@ int main(void)
             }
         }
     }
-    printf("logf restated vs glibc on all 2^31 non-negative floats: %ld mismatches (separate), %ld (fused)\n",
-           bad[0], bad[1]);
+    printf("logf restated vs glibc on every %llu-th of the 2^31 non-negative floats: %ld mismatches (separate), "
+           "%ld (fused)\n", (unsigned long long)(step ? step : 1), bad[0], bad[1]);
     return bad[0] || bad[1];
 }
