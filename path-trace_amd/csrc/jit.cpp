@@ -87,6 +87,11 @@ const char *kOptions[] = {
      * C2 and C5 unchanged within noise) */
     "-mllvm",
     "-split-spill-mode=size",
+    /* no unclustered high-register-pressure rescheduling stage: same-box A/B,
+     * profiles/round4/ab_sched_options_*.txt: C2 +1.4 %, C5 +0.1 %, C3 +-0
+     * (max-ilp scheduling: C3 -5.5 %; the AMDGPU RP trackers: +-0.5 %) */
+    "-mllvm",
+    "-amdgpu-disable-unclustered-high-rp-reschedule",
     /* LDS is sized by hand for the workgroups-per-CU target (min_workgroups);
      * private arrays the promoter would move into spare LDS can push a
      * workgroup past the CU's 160 KB / 1280-B granule budget */
