@@ -252,8 +252,12 @@ Generated generate(const SceneImpl &s, int depth)
     /* Difference-free trees skip a sphere's root and divisions when no lane of
      * the wave meets it (pt_device.h PT_SPHERE_SKIP; same-box A/B,
      * profiles/round4/ab_sphere_skip.txt: C2 +7.2 %, C5 +0.3 %, C3 -10 %) */
+    /* ... and run generation rounds of 6 attempts per lane (C2 +1.7 % over 8,
+     * 4 of 4 reps on one box, profiles/round4/ab_katt_c2_fixed.txt; 4: -0.9 %;
+     * C3 lost 9 % at 6 in round 3) */
     if (root.find("Diff<") == std::string::npos)
-        src << "#ifndef PT_SPHERE_SKIP\n#define PT_SPHERE_SKIP 1\n#endif\n";
+        src << "#ifndef PT_SPHERE_SKIP\n#define PT_SPHERE_SKIP 1\n#endif\n"
+            << "#ifndef PT_KATT\n#define PT_KATT 6\n#endif\n";
     /* experiment hook: A/B a different device library text in the same run,
      * e.g. PT_DEVICE_HEADER=tools/ab/old.h (profiling only) */
     if (const char *hdr = getenv("PT_DEVICE_HEADER")) {

@@ -1985,8 +1985,9 @@ __device__ __forceinline__ void cadd(u64 &c, u32 v)
 
 /* LCG jumps in LDS, shared by the workgroup's waves: j3[l] = (A, G * inc) of
  * 3l draws (attempt l of a round, lane l in attempt-major rounds; k < 8: the
- * offset of a lane-major round's k-th attempt), j24[l] = the same for 24l
- * draws (lane l's first attempt, 8l, in a lane-major round).  Read where a
+ * offset of a lane-major round's k-th attempt), j24[l] = the same for
+ * 3 PT_KATT l draws (lane l's first attempt, PT_KATT l, in a lane-major
+ * round; 24l at the default 8).  Read where a
  * round needs them: hoisted out of the burst loop they would be held in
  * registers and spilled to scratch. */
 struct JumpLds
@@ -3799,7 +3800,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     }
 #endif
     for (int i = threadIdx.x; i < 128; i += 64 * PT_WPW) {
-        const int l = i & 63, m = i < 64 ? l : 8 * l; /* m attempts = 3m draws */
+        const int l = i & 63, m = i < 64 ? l : PT_KATT * l; /* m attempts = 3m draws */
         u64 *t = i < 64 ? jbuf[l] : jbuf24[l];
         t[0] = jump[2 * m], t[1] = jump[2 * m + 1] * LCG_INC;
     }
