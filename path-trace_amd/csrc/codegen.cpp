@@ -258,6 +258,10 @@ Generated generate(const SceneImpl &s, int depth)
     if (root.find("Diff<") == std::string::npos)
         src << "#ifndef PT_SPHERE_SKIP\n#define PT_SPHERE_SKIP 1\n#endif\n"
             << "#ifndef PT_KATT\n#define PT_KATT 6\n#endif\n";
+    /* trees with a Difference and no lane walks (C3): 10 attempts per lane
+     * (+1.1 %, 3 of 3 reps, profiles/round4/ab_katt_c3.txt; 6: -5.4 %) */
+    else if (s.lane_walk == 0 && !s.lane_scatter)
+        src << "#ifndef PT_KATT\n#define PT_KATT 10\n#endif\n";
     /* experiment hook: A/B a different device library text in the same run,
      * e.g. PT_DEVICE_HEADER=tools/ab/old.h (profiling only) */
     if (const char *hdr = getenv("PT_DEVICE_HEADER")) {
