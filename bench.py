@@ -40,9 +40,11 @@ VALU_PEAK_TOPS = 78.6  # 256 CU x 128 FP32 lanes/clk x 2.4 GHz, no FMA (contract
 # counts on hashed pixels): C3 8192 px x 32 spp, C2 512 px x 4 spp, C5 8192 px x 64 spp
 # (C5's texture work -- spherical/skybox maps -- is outside the op model)
 OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 614.78, "C5": 554.13}
-# Counter evidence of this same command (tools/pmc_bench.sh: rocprofv3 --pmc
-# passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 + WRITE_SIZE)
-PMC_JSON = os.path.join(ROOT, "profiles", "round4", "pmc_bench_%s.json")
+# Counter evidence of this same command (tools/evidence.sh -> tools/pmc_bench.sh:
+# rocprofv3 --pmc passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 +
+# WRITE_SIZE).  Each file records the code-object key of the kernel its passes
+# ran; the line attaches it only when that key is the key of the kernel it timed.
+PMC_JSON = os.path.join(ROOT, "profiles", "round5", "pmc_bench_%s.json")
 # bounded CPU samples at full spp on the box's per-GPU CPU share (16 threads):
 # BASELINE.md's 4096 hashed pixels (C3: ~60 s), fewer where a pixel costs more
 CPU_PIXELS = {"C1": 4096, "C2": 512, "C3": 4096, "C4": 1024, "C5": 32768}
@@ -55,12 +57,19 @@ CPU_PIXELS = {"C1": 4096, "C2": 512, "C3": 4096, "C4": 1024, "C5": 32768}
 SUBSET_1GPU = {"C5": 65536}
 
 
-def pmc_evidence(cfg_name: str):
+def pmc_evidence(cfg_name: str, kernel_key: str):
+    """(PMC summary, None) when profiles/.../pmc_bench_<cfg>.json was collected
+    on the code object just timed, else (None, why not)."""
+    path = PMC_JSON % cfg_name
     try:
-        with open(PMC_JSON % cfg_name) as f:
-            return json.load(f)
+        with open(path) as f:
+            ev = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, "no counter file %s" % os.path.relpath(path, ROOT)
+    if ev.get("kernel_key") != kernel_key:
+        return None, "%s was collected on code object %s, not on the timed %s" % (
+            os.path.relpath(path, ROOT), ev.get("kernel_key"), kernel_key)
+    return ev, None
 
 
 def parse():
@@ -83,6 +92,9 @@ def parse():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="N>1: RCCL over xGMI (nccl), or gloo with the frame reduced through host memory -- "
                          "rehearses the N>1 code path with several ranks on one GPU")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the N > 1 step at any world size: torch.distributed over RCCL (a one-rank group "
+                         "when launched without torchrun), per-pixel sums, the device reduce, rank 0's division")
     ap.add_argument("--split", choices=["samples", "tiles"], default="samples",
                     help="N>1: each rank renders every pixel for its share of the samples (balanced to noise), "
                          "or the hashed 16x16 tiles it owns (bit-identical to 1 GPU, measured 1.19 max/mean "
@@ -162,12 +174,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    gloo = world > 1 and args.backend == "gloo"
+    use_dist = world > 1 or args.force_dist
+    gloo = use_dist and args.backend == "gloo"
     if gloo:  # rehearsal: ranks may share a GPU
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:
+    if use_dist:
         import torch.distributed as dist
+        if "MASTER_ADDR" not in os.environ:  # --force-dist without torchrun: a one-rank group
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
         if gloo:
             dist.init_process_group("gloo")
         else:
@@ -188,7 +207,8 @@ def main():
     # this rank's share (pathtrace.dist.RankFrame, also driven by tests/test_dist_gpu.py)
     share = ptdist.RankFrame(ds, W, H, spp, cfg.depth, rank=rank, world=world, split=args.split,
                              screen=cfg.screen, subset=keep, order=args.order, device=local,
-                             max_buffer_bytes=40 << 30)
+                             max_buffer_bytes=40 << 30, force_split=use_dist)
+    kernel_key = ds.kernel_key(cfg.depth)
     by_samples, mine = share.by_samples, share.pixels
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream()
@@ -232,7 +252,7 @@ def main():
     kernel_ms = st["kernel_ms"] / max(1, st["launches"])
     launches_per_step = st["launches"] // max(1, args.steps)
     queries = st["queries"]
-    if dist is not None:
+    if dist is not None:  # RCCL: CUDA tensors; gloo: host tensors
         dev = "cpu" if gloo else "cuda"
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -253,6 +273,7 @@ def main():
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 1), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "kernel_key": kernel_key,
             "config": {"workload": "%s: %dx%d, %d spp, depth %d, %s%s" % (
                 cfg.name, W, H, spp, cfg.depth, cfg.note,
                 ("; timed on %d hashed pixels at full spp" % subset) if subset else ""),
@@ -262,7 +283,9 @@ def main():
                                     ("every pixel, spp split over ranks, per-pixel sums" if by_samples
                                      else "16x16 tiles hashed over ranks") +
                                     (" + gloo reduce through host memory (rehearsal: %d ranks on %d GPU(s))" %
-                                     (world, torch.cuda.device_count()) if gloo else " + RCCL reduce"))},
+                                     (world, torch.cuda.device_count()) if gloo else " + RCCL reduce")) +
+                                   (" (--force-dist: the N > 1 step at world size %d)" % world
+                                    if args.force_dist else "")},
             "samples_per_step": npix_total * spp,
             "queries_per_sample": round(queries / samples, 2),
         }
@@ -271,14 +294,17 @@ def main():
             ops_per_launch = opq * queries / (args.steps * launches_per_step * world)
             achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12
             # the PMC passes ran this same command at N = 1 (config defaults: C5's subset, fast order)
-            same = world == 1 and args.subset < 0 and not args.spp and args.order == "fast"
-            ev = pmc_evidence(cfg.name) if same else None
+            same = world == 1 and args.subset < 0 and not args.spp and args.order == "fast" and not use_dist
+            ev, why = pmc_evidence(cfg.name, kernel_key) if same else (
+                None, "counters are collected on the default one-GPU command only")
             out["roofline"] = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS,
                                "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
                                "traffic": round(ev["hbm_bytes_per_launch"]) if ev else None,
-                               "kernel": "pt_render_fast", "avg_launch_ms": round(kernel_ms, 2),
-                               "ops_per_query": opq}
-            if ev:
+                               "kernel": "pt_render_fast", "kernel_key": kernel_key,
+                               "avg_launch_ms": round(kernel_ms, 2), "ops_per_query": opq}
+            if not ev:
+                out["roofline"]["traffic_note"] = why
+            else:
                 out["roofline"].update({
                     "traffic_unit": "HBM bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE, %s)" %
                                     os.path.relpath(PMC_JSON % cfg.name, ROOT),

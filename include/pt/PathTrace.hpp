@@ -769,9 +769,22 @@ inline FrameEngine &defaultFrameEngine()
 /* tracePixel(SpanIterator &, int px, int py, ...) of include/path-trace.h:187-201
  * over a batch: colors[k] = the mean radiance of pixel (px[k], py[k]).  The span
  * iterator must be a built-in object's (Object::makeSpanIterator): its object is
- * the scene the device renders.  One device launch for the whole batch.
- * Pixels past the right edge (the adaptive caller's block corners at x ==
- * screenXResolution, src/test.cpp:466-499) are keyed on a grid one wider. */
+ * the scene the device renders.  One device launch for the in-frame pixels.
+ * A pixel's engine keys depend on the pixel alone, never on the rest of the
+ * batch: pixels with x < screenXResolution are keyed on the frame's grid (the
+ * bits Renderer::render returns); pixels past the right edge (the adaptive
+ * caller's block corners at x == screenXResolution, src/test.cpp:466-499) are
+ * rendered per column x in a launch of their own, keyed on a grid x + 1 wide
+ * with a run seed derived from (engine.seed, x), so they can share no sample
+ * stream with an in-frame pixel. */
+inline uint64_t edgeColumnSeed(uint64_t seed, int x)
+{
+    uint64_t z = seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(uint32_t)(x + 1));
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
 inline void tracePixels(SpanIterator &spanIterator, const int32_t *px, const int32_t *py, size_t n, Color *colors,
                         int screenXResolution, int screenYResolution, int sampleCount, int rayDepth, float screenWidth,
                         float screenHeight, float screenDistance, const FrameEngine &engine)
@@ -782,24 +795,41 @@ inline void tracePixels(SpanIterator &spanIterator, const int32_t *px, const int
                                       "(Object::makeSpanIterator)");
     if (n == 0)
         return;
-    int gw = screenXResolution;
+    static_assert(sizeof(Color) == 3 * sizeof(float), "Color must be 3 packed floats");
+    const int W = screenXResolution;
+    std::vector<int32_t> in_pix;
+    std::vector<size_t> in_at;
+    std::map<int, std::vector<size_t>> edge; /* column x >= W -> batch positions */
     for (size_t k = 0; k < n; k++) {
         if (px[k] < 0 || py[k] < 0)
             throw std::invalid_argument("tracePixel: negative pixel coordinate");
-        if (px[k] >= gw)
-            gw = px[k] + 1;
-    }
-    std::vector<int32_t> pix(n);
-    for (size_t k = 0; k < n; k++) {
+        const int gw = px[k] < W ? W : px[k] + 1;
         const int64_t i = (int64_t)py[k] * gw + px[k];
         if (i > INT32_MAX)
             throw std::invalid_argument("tracePixel: pixel index out of range");
-        pix[k] = (int32_t)i;
+        if (px[k] < W) {
+            in_pix.push_back((int32_t)i);
+            in_at.push_back(k);
+        } else {
+            edge[px[k]].push_back(k);
+        }
     }
-    static_assert(sizeof(Color) == 3 * sizeof(float), "Color must be 3 packed floats");
-    it->renderPixels(pix.data(), (int64_t)n, screenXResolution, screenYResolution, gw, sampleCount, rayDepth,
-                     screenWidth, screenHeight, screenDistance, engine.seed, engine.order,
-                     reinterpret_cast<float *>(colors));
+    std::vector<float> rgb;
+    auto launch = [&](const std::vector<int32_t> &pix, const std::vector<size_t> &at, int gw, uint64_t seed) {
+        rgb.assign(3 * pix.size(), 0.0f);
+        it->renderPixels(pix.data(), (int64_t)pix.size(), W, screenYResolution, gw, sampleCount, rayDepth,
+                         screenWidth, screenHeight, screenDistance, seed, engine.order, rgb.data());
+        for (size_t j = 0; j < at.size(); j++)
+            colors[at[j]] = Color(rgb[3 * j], rgb[3 * j + 1], rgb[3 * j + 2]);
+    };
+    if (!in_pix.empty())
+        launch(in_pix, in_at, W, engine.seed);
+    for (const auto &col : edge) {
+        std::vector<int32_t> pix;
+        for (size_t k : col.second)
+            pix.push_back((int32_t)((int64_t)py[k] * (col.first + 1) + col.first));
+        launch(pix, col.second, col.first + 1, edgeColumnSeed(engine.seed, col.first));
+    }
 }
 
 inline Color tracePixel(SpanIterator &spanIterator, int px, int py, int screenXResolution, int screenYResolution,

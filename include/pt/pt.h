@@ -246,7 +246,9 @@ int pt_scene_set_lane_walk(pt_scene *s, int frames);
  * dozen leaves each); supersedes pt_scene_set_lane_walk.  Takes effect at the
  * next compile/render. */
 int pt_scene_set_lane_scatter(pt_scene *s, int on);
-/* Key of the code object for this scene/depth (hex string, static storage). */
+/* Key of the code object for this scene/depth: a hash of the generated source,
+ * the compiler options and the hiprtc version -- the file name of its entry in
+ * the code-object cache (hex string, thread-local storage). */
 const char *pt_scene_kernel_key(pt_scene *s, int depth);
 
 /* ------------------------------------------------------------ queries --- */

@@ -87,7 +87,7 @@ struct SceneImpl
 struct Generated
 {
     std::string source;         /* full hiprtc translation unit                      */
-    std::string key;            /* content hash of source + options + compiler        */
+    std::string key;            /* content hash of the source (code_object_key adds options + compiler) */
     std::vector<float> params;  /* scene parameter block P                           */
     std::vector<int> image_ids; /* slot -> scene image index                          */
     std::vector<int> mat_ids;   /* compact material index -> scene material index     */
@@ -101,6 +101,9 @@ Generated generate(const SceneImpl &s, int depth);
 Generated generate_query(const SceneImpl &s, int obj, int tex);
 /* Returns the gfx950 code object for g (from the cache or compiled now). */
 const std::vector<char> &code_object(const Generated &g);
+/* The code object's cache key: source + compiler options + hiprtc version
+ * (the _jit_cache file name; what a profile is bound to). */
+std::string code_object_key(const Generated &g);
 
 /* Matrix helpers (reference include/transform.h arithmetic). */
 void mat_inverse(const float *m, float *out); /* throws Error(PT_ERR_MATH) */

@@ -193,6 +193,8 @@ std::vector<char> compile(const Generated &g, std::string &log)
 
 } // namespace
 
+std::string code_object_key(const Generated &g) { return full_key(g); }
+
 const std::vector<char> &code_object(const Generated &g)
 {
     std::lock_guard<std::mutex> lk(g_mu);

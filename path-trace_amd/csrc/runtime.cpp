@@ -1282,7 +1282,7 @@ const char *pt_scene_kernel_key(pt_scene *s, int depth)
 {
     thread_local std::string k;
     try {
-        k = generate(S(s), depth).key;
+        k = code_object_key(generate(S(s), depth));
     } catch (std::exception &e) {
         set_error(e.what());
         k.clear();

@@ -172,6 +172,14 @@ class DeviceScene:
             tid = int(t) if isinstance(t, (int, np.integer)) else self._tex(t)
             _lib.check(_lib.lib().pt_query_compile(self._h, -2, tid))
 
+    def kernel_key(self, depth: int) -> str:
+        """The code-object key of this scene's render kernel at `depth`
+        (pt_scene_kernel_key: source + compiler options + hiprtc version)."""
+        k = _lib.lib().pt_scene_kernel_key(self._h, depth).decode()
+        if not k:
+            raise PtError(_lib.lib().pt_last_error().decode())
+        return k
+
     def compile(self, depth: int) -> str:
         _lib.check(_lib.lib().pt_scene_compile(self._h, depth))
         return _lib.lib().pt_scene_kernel_key(self._h, depth).decode()

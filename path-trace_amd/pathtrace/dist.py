@@ -61,12 +61,14 @@ class RankFrame:
     the single-GPU frame bit for bit.  One rank is the plain full render."""
 
     def __init__(self, ds, width, height, spp, depth, rank=0, world=1, split="samples", screen=None,
-                 subset=None, order="fast", device=0, max_buffer_bytes=0, seed=0x5EED):
+                 subset=None, order="fast", device=0, max_buffer_bytes=0, seed=0x5EED, force_split=False):
         from . import make_params
         if split not in ("samples", "tiles"):
             raise ValueError("split must be 'samples' or 'tiles'")
         self.ds, self.rank, self.world, self.spp, self.device = ds, rank, world, spp, device
-        self.by_samples = world > 1 and split == "samples"
+        # force_split: take the N > 1 path even for one rank (per-pixel sums +
+        # the reduce + rank 0's division), e.g. bench.py --force-dist
+        self.by_samples = (world > 1 or force_split) and split == "samples"
         mine = rank_pixels(width, height, rank, 1 if self.by_samples else world)
         if subset is not None:
             mine = np.intersect1d(mine, np.asarray(subset)).astype(np.int32)

@@ -24,14 +24,14 @@ def _free_port():
     return port
 
 
-def _bench(args, nproc, tmp_path, name):
+def _bench(args, nproc, tmp_path, name, env_extra=None):
     frame = str(tmp_path / (name + ".npy"))
     cmd = [sys.executable, "-u"]
     if nproc > 1:
         cmd += ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port())]
     cmd += [os.path.join(ROOT, "bench.py"), "--gpus", str(nproc)] + args + ["--dump-frame", frame]
-    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env = dict(os.environ, OMP_NUM_THREADS="4", **(env_extra or {}))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -42,13 +42,15 @@ def _bench(args, nproc, tmp_path, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("split", ["samples", "tiles"])
 def test_bench_two_ranks_gloo(tmp_path, split):
-    common = ["--config", "C3", "--spp", "64", "--steps", "1", "--warmup", "0", "--cpu-pixels", "64"]
+    # 256 spp: each of the two ranks renders 128 samples per pixel, so it takes the
+    # block-staged path (whole 32-sample blocks) a real rank share takes
+    common = ["--config", "C3", "--spp", "256", "--steps", "1", "--warmup", "0", "--cpu-pixels", "16"]
     one, f1 = _bench(common + ["--no-cpu"], 1, tmp_path, "one")
     two, f2 = _bench(common + ["--backend", "gloo", "--split", split], 2, tmp_path, "two")
     assert two["n_gpus"] == 2 and two["steps"] == 1
     assert "gloo reduce" in two["config"]["sharding"]
     assert ("spp split" in two["config"]["sharding"]) == (split == "samples")
-    assert two["samples_per_step"] == one["samples_per_step"] == 1920 * 1080 * 64
+    assert two["samples_per_step"] == one["samples_per_step"] == 1920 * 1080 * 256
     # the same frame: the same span queries in total, split over the ranks
     assert two["queries_per_sample"] == pytest.approx(one["queries_per_sample"], rel=1e-9)
     # roofline: each rank's launches carry half the work; the kernel time is the max over ranks
@@ -64,3 +66,22 @@ def test_bench_two_ranks_gloo(tmp_path, split):
     else:  # the ranks' partial sums change the association only
         rmse = np.sqrt(np.mean((f2.astype(np.float64) - f1) ** 2, axis=(0, 1)))
         assert rmse.max() <= 1e-6, rmse
+
+
+@pytest.mark.gpu
+def test_bench_force_dist_rccl_world1(tmp_path):
+    """the RCCL leg of bench.py executed -- init_process_group("nccl",
+    device_id=...), the device dist.reduce of the frame, the CUDA-tensor MAX / SUM
+    all-reduces and rank 0's division -- as a one-rank group on one GPU.  The
+    rank renders per-pixel sums (sum_only) and the frame after the reduce and the
+    division by spp is the plain one-GPU frame bit for bit (the kernel's mean is
+    the same sum divided by the same spp)."""
+    common = ["--config", "C3", "--spp", "64", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    one, f1 = _bench(common, 1, tmp_path, "plain")
+    d, f2 = _bench(common + ["--force-dist"], 1, tmp_path, "rccl")
+    assert d["n_gpus"] == 1 and d["steps"] == 2
+    assert "RCCL reduce" in d["config"]["sharding"] and "force-dist" in d["config"]["sharding"]
+    assert d["samples_per_step"] == one["samples_per_step"]
+    assert d["queries_per_sample"] == pytest.approx(one["queries_per_sample"], rel=1e-9)
+    assert d["roofline"]["traffic"] is None and "default one-GPU command" in d["roofline"]["traffic_note"]
+    np.testing.assert_array_equal(f2.view(np.uint32), f1.view(np.uint32))

@@ -38,12 +38,17 @@ def bench_line(name):
 busy, fetch, write = counters("busy"), counters("fetch"), counters("write")
 stall, cache, tex = counters("stall"), counters("cache"), counters("tex")
 b = bench_line("busy")
+# the code object every pass ran (bench.py attaches this file only to a line that timed the same one)
+keys = {bench_line(n).get("kernel_key") for n in ("busy", "fetch", "write", "stall", "cache", "tex")}
+if len(keys) != 1 or None in keys:
+    raise SystemExit("passes ran different or unknown code objects: %s" % sorted(map(str, keys)))
 launches = b["steps"]  # one render launch per step at the bench config (one pass)
 samples = b["value"] * 1e6 * b["ms_per_step"] * 1e-3 * b["steps"]
 kernel_s = b["roofline"]["avg_launch_ms"] * 1e-3 if "roofline" in b else None
 gui = busy["GRBM_GUI_ACTIVE"] / XCDS
 res = {
-    "kernel": "pt_render_fast", "workload": b["config"]["workload"], "bench_value": b["value"],
+    "kernel": "pt_render_fast", "kernel_key": b["kernel_key"], "workload": b["config"]["workload"],
+    "bench_value": b["value"], "avg_launch_ms": b["roofline"]["avg_launch_ms"],
     "valu_busy": busy["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / gui,
     # > 1 here: SQ_ACTIVE_INST_VALU is summed over waves, and several waves'
     # VALU instructions are in flight on one SIMD at once, so also report the
