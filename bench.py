@@ -279,7 +279,7 @@ def main():
                 ("; timed on %d hashed pixels at full spp" % subset) if subset else ""),
                        "order": args.order,
                        "sharding": (("one GPU renders every pixel" if not subset else
-                                     "one GPU renders %d hashed pixels of the frame" % subset) if world == 1 else
+                                     "one GPU renders %d hashed pixels of the frame" % subset) if not use_dist else
                                     ("every pixel, spp split over ranks, per-pixel sums" if by_samples
                                      else "16x16 tiles hashed over ranks") +
                                     (" + gloo reduce through host memory (rehearsal: %d ranks on %d GPU(s))" %

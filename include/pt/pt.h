@@ -205,6 +205,31 @@ typedef struct pt_adaptive_params {
 int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_params *ap, float *rgb_out,
                        pt_render_stats *stats);
 
+/* traceRay<T>(const Ray &ray, SpanIterator &, int depth, T &engine, float
+ * strength) of include/path-trace.h:58-165 for a batch of caller rays, in one
+ * device launch.  rays = n records of 7 floats: origin xyz, direction xyz
+ * (non-zero: Ray's assert, include/ray.h:17; not normalised), strength.
+ * rgb_out receives, per ray, the mean of spp traceRay samples -- sample s of ray
+ * k drawing from the engine keyed (seed, k, sample_begin + s), include/pt/
+ * pt_engine.h -- summed in `order` and divided by spp: with spp = 1 the
+ * traceRay value itself (as (0 + c) / 1: a -0 channel reads +0), with the
+ * camera ray of a point and spp = sampleCount tracePixel's float-coordinate
+ * overload (path-trace.h:172-185). */
+typedef struct pt_trace_params {
+    int spp;                       /* samples per ray (>= 1)                                    */
+    int depth;                     /* rayDepth                                                  */
+    uint64_t seed;                 /* run seed of the per-(ray, sample) engine                  */
+    int order;                     /* PT_ORDER_*                                                */
+    int device;                    /* HIP device ordinal                                        */
+    int sample_begin;              /* engine sample index of the first sample                   */
+    int64_t max_buffer_bytes;      /* per-sample staging budget (0 = 8 GiB)                     */
+} pt_trace_params;
+int pt_trace_rays(pt_scene *s, const pt_trace_params *p, const float *rays, int64_t n, float *rgb_out,
+                  pt_render_stats *stats);
+/* JIT-compile (or fetch from the cache) pt_trace_rays' module for this scene
+ * and depth without touching a GPU. */
+int pt_trace_compile(pt_scene *s, int depth);
+
 /* Everything a render with p needs -- code object loaded, scene parameters
  * and images uploaded, staging buffers allocated -- without rendering, so a
  * timed or latency-sensitive render does no compilation or allocation. */

@@ -1293,6 +1293,53 @@ int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int 
     }
 }
 
+/* traceRay<T>(ray, it, depth, engine, strength), include/path-trace.h:58-165,
+ * for n caller rays (7 floats: origin, direction, strength): per ray the sum of
+ * spp samples in `order` (pixel_sum), sample s drawing from the engine keyed
+ * (seed, ray index, sample_begin + s), each sample (0 + c) / 1 as a one-sample
+ * tracePixel adds it, divided by spp -- what pt_trace_rays computes. */
+int oracle_trace_rays(const char *scene_text, const float *rays, int n, int spp, int depth, uint64_t seed,
+                      int sample_begin, int threads, int order, float *out)
+{
+    try {
+        std::unique_ptr<Scene> scene = load_scene(scene_text);
+        std::atomic<int> next(0);
+        std::mutex mu;
+        std::string err;
+        auto worker = [&]() {
+            Tracer<SampleEngine> tr(*scene, order == 1 ? ORDER_FAST : ORDER_REFERENCE);
+            try {
+                for (;;) {
+                    int k = next.fetch_add(1);
+                    if (k >= n)
+                        break;
+                    const float *r = rays + 7 * (size_t)k;
+                    const Ray ray{V3(r[0], r[1], r[2]), V3(r[3], r[4], r[5])};
+                    V3 acc = pixel_sum(spp, order == 1 ? ORDER_FAST : ORDER_REFERENCE, [&](int s) {
+                        SampleEngine e(seed, (uint64_t)k, (uint64_t)(sample_begin + s));
+                        V3 c = V3(0, 0, 0) + tr.trace(ray, depth, e, r[6]);
+                        return c / (float)1;
+                    });
+                    acc = acc / (float)spp;
+                    out[3 * (size_t)k + 0] = acc.x, out[3 * (size_t)k + 1] = acc.y, out[3 * (size_t)k + 2] = acc.z;
+                }
+            } catch (std::exception &e) {
+                std::lock_guard<std::mutex> g(mu);
+                err = e.what();
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 0; t < (threads < 1 ? 1 : threads); t++) pool.emplace_back(worker);
+        for (auto &t : pool) t.join();
+        if (!err.empty())
+            throw std::runtime_error(err);
+        return 0;
+    } catch (std::exception &e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
 /* Full root span list per ray; layout as ptref's "spans" mode:
  * int32 count, then count * (t0 n0.xyz m0 t1 n1.xyz m1) with m as int32. */
 int oracle_spans(const char *scene_text, const float *rays, int n, char *out, int64_t cap, int64_t *written)

@@ -62,6 +62,9 @@ def lib():
         L.oracle_render_adaptive.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float,
                                              C.c_float, C.c_uint64, C.c_int, C.c_int, C.c_float, C.c_int, C.c_int,
                                              C.c_void_p, C.c_void_p]
+        L.oracle_trace_rays.restype = C.c_int
+        L.oracle_trace_rays.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int,
+                                        C.c_int, C.c_int, C.c_void_p]
         L.oracle_kat.restype = ctypes.c_int
         L.oracle_kat.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         _lib = L
@@ -118,6 +121,35 @@ def render_adaptive(scene_text: str, W: int, H: int, spp: int, depth: int, block
     if rc != 0:
         raise RuntimeError("oracle_render_adaptive: " + L.oracle_last_error().decode())
     return out, int(traced[0])
+
+
+def trace_rays(scene_text: str, rays: np.ndarray, spp: int, depth: int, seed: int = 0x5EED, sample_begin: int = 0,
+               threads: int = 0, order: int = ORDER_REFERENCE):
+    """traceRay per caller ray (n x 7: origin, direction, strength): the mean
+    of spp samples keyed (seed, ray, sample) -- pt_trace_rays' restatement."""
+    r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 7)
+    out = np.zeros((len(r), 3), dtype=np.float32)
+    rc = lib().oracle_trace_rays(scene_text.encode(), r.ctypes.data, len(r), spp, depth, seed, sample_begin,
+                                 threads or (os.cpu_count() or 1), order, out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("oracle_trace_rays: " + lib().oracle_last_error().decode())
+    return out
+
+
+def ref_trace_rays(scene_text: str, rays: np.ndarray, spp: int, depth: int, seed: int = 0x5EED,
+                   threads: int = 0):
+    """The same from the unmodified reference (ptref "rays" mode:
+    PathTrace::traceRay<PtSampleEngine> per (ray, sample), summed in order)."""
+    r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 7)
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "scene.txt")
+        with open(sp, "w") as f:
+            f.write(scene_text)
+        rp = os.path.join(td, "rays.bin")
+        r.tofile(rp)
+        op = os.path.join(td, "out.bin")
+        _ref(["rays", sp, rp, str(spp), str(depth), str(seed), str(threads or (os.cpu_count() or 1)), op])
+        return np.fromfile(op, dtype=np.float32).reshape(len(r), 3)
 
 
 def _parse_spans(buf: bytes, n: int):

@@ -19,6 +19,10 @@
  * Modes (argv[1]):
  *   render  scene.txt W H spp depth sw sh dist seed pixels.bin|all threads per_sample out.bin
  *   spans   scene.txt rays.bin out.bin       full span list of root for each ray
+ *   rays    scene.txt rays.bin spp depth seed threads out.bin
+ *           traceRay<PtSampleEngine>(ray, it, depth, engine, strength) (path-trace.h:58-165)
+ *           per (ray, sample) of rays.bin (n * 7 floats: origin, dir, strength),
+ *           Color(0,0,0) + traceRay, summed in sample order, / spp
  *   tex     scene.txt points.bin out.bin     getColor / getFloat of every texture at each point
  *   kat     out.bin                          engine / math known-answer vectors
  *   hdr     in.hdr out_rgba.bin out_rewritten.hdr   reference HDR read + writeHDR
@@ -250,6 +254,50 @@ int mode_render(int argc, char **argv)
     return 0;
 }
 
+int mode_rays(int argc, char **argv)
+{
+    if (argc != 9) {
+        fprintf(stderr, "rays: bad args\n");
+        return 2;
+    }
+    std::vector<char> txt = read_file(argv[2]);
+    scenetext::Desc d = scenetext::parse(std::string(txt.data(), txt.size()));
+    World w;
+    build_world(d, w);
+    std::vector<char> raw = read_file(argv[3]);
+    const float *r = (const float *)raw.data();
+    const size_t n = raw.size() / 28;
+    const int spp = atoi(argv[4]), depth = atoi(argv[5]), threads = atoi(argv[7]);
+    const unsigned long long seed = strtoull(argv[6], nullptr, 0);
+    std::vector<float> result(n * 3);
+    std::atomic<size_t> next(0);
+    auto worker = [&]() {
+        std::unique_ptr<SpanIterator> it(w.root->makeSpanIterator());
+        for (;;) {
+            size_t k = next.fetch_add(1);
+            if (k >= n)
+                break;
+            const float *q = r + 7 * k;
+            Ray ray(Vector3D(q[0], q[1], q[2]), Vector3D(q[3], q[4], q[5]));
+            Color acc(0, 0, 0);
+            for (int s = 0; s < spp; s++) {
+                PtSampleEngine e((uint64_t)seed, (uint64_t)k, (uint64_t)s);
+                Color c = Color(0, 0, 0);
+                c += traceRay(ray, *it, depth, e, q[6]);
+                c /= 1;
+                acc += c;
+            }
+            acc /= spp;
+            result[3 * k] = acc.x, result[3 * k + 1] = acc.y, result[3 * k + 2] = acc.z;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; t++) pool.emplace_back(worker);
+    for (auto &t : pool) t.join();
+    write_file(argv[8], result.data(), result.size() * 4);
+    return 0;
+}
+
 /* spans: rays.bin = n * 6 floats (origin, dir).  out.bin per ray: int32 count,
  * then count * (start, sN.xyz, sMat, end, eN.xyz, eMat) as 10 x 4 bytes. */
 int mode_spans(int argc, char **argv)
@@ -471,6 +519,8 @@ int main(int argc, char **argv)
             return mode_render(argc, argv);
         if (m == "spans")
             return mode_spans(argc, argv);
+        if (m == "rays")
+            return mode_rays(argc, argv);
         if (m == "kat")
             return mode_kat(argc, argv);
         if (m == "hdr")

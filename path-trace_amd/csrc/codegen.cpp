@@ -177,7 +177,7 @@ uint64_t fnv1a(const std::string &s, uint64_t h = 1469598103934665603ull)
 
 } // namespace
 
-Generated generate(const SceneImpl &s, int depth)
+Generated generate(const SceneImpl &s, int depth, bool rays)
 {
     if (s.root < 0)
         throw Error(PT_ERR_ARG, "scene has no root object (pt_set_root)");
@@ -237,6 +237,9 @@ Generated generate(const SceneImpl &s, int depth)
             src << "#define " << (eq == std::string::npos ? d : d.substr(0, eq) + " " + d.substr(eq + 1)) << "\n";
         }
     }
+    /* the ray-list module of pt_trace_rays: items are caller rays, not camera samples */
+    if (rays)
+        src << "#define PT_RAYS 1\n";
     /* per-scene occupancy (pt_scene_set_occupancy): the launch bounds' workgroups per CU */
     if (s.wg_per_cu > 0)
         src << "#define PT_MIN_WAVES " << s.wg_per_cu << "\n";

@@ -78,6 +78,9 @@ struct PtLaunch
                            per sample */
     long long perm;     /* sample-major: slot = (k * perm) mod nslots for the k-th
                            slot of a sample (perm coprime to nslots; 0 = k)      */
+    const float *rays;  /* PT_RAYS modules (pt_trace_rays): slot k's ray, 7 floats
+                           (origin, direction, strength) -- traceRay's arguments,
+                           include/path-trace.h:59 -- instead of a camera ray    */
 };
 
 struct Env
@@ -2150,6 +2153,8 @@ enum { B_DONE = 0, B_ABORT = 1, B_NONLEAF = 2 };
 static_assert(PT_KATT % 2 == 0, "deferred rounds evaluate attempts in pairs");
 #define PT_JUMP_ENTRIES 1025 /* host table: m = 0..1024 attempts */
 static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
+/* lane-major rounds count a lane's trailing failures in 4 balloted bit planes */
+static_assert(PT_KATT <= 15, "a lane's trailing-failure count must fit 4 bits");
 
 /* One rejection attempt of the scatter loop body (path-trace.h:141-158):
  * s0 is the engine state before the attempt's three draws (outputs of s1, s2, s3). */
@@ -3029,10 +3034,10 @@ __device__ __forceinline__ V3 camera_dir(const PtLaunch &lp, int pix, Rng &rng)
  * returns false, leaving the sample to the wave, for any other shape.
  * nq / nsh = queries / shaded hits, for the statistics. */
 template <class S>
-__device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 d, const CamHit &ch, V3 &res, int &nq,
-                                            int &nsh)
+__device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 o, V3 d, float strength, const CamHit &ch,
+                                            V3 &res, int &nq, int &nsh)
 {
-    const V3 z = mk(0, 0, 0), o = mk(0, 0, 0);
+    const V3 z = mk(0, 0, 0);
     nq = 1, nsh = 0;
     if (!ch.hit) {
         res = (z + mk(0, 0, 0)) / 1.0f;
@@ -3053,8 +3058,8 @@ __device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 d, const
         ior = (float)(1.0 / (double)S::ior(mat, e));
     }
     const V3 retval = S::emis(mat, hit, e);
-    const float strength = 1.0f, add = 1.0f;
-    if (depth <= 0) {
+    const float add = 1.0f;
+    if (depth <= 0 || strength < EPS) {
         res = (z + retval) / 1.0f;
         return true;
     }
@@ -3107,8 +3112,8 @@ struct WalkFrame
     int mdep;          /* its depth */
 };
 template <class S>
-__device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 d0, const CamHit &ch, V3 &res, int &nq,
-                                          int &nsh)
+__device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 o0, V3 d0, float str0, const CamHit &ch,
+                                          V3 &res, int &nq, int &nsh)
 {
     constexpr int K = PT_LANE_WALK;
     WalkFrame F[K];
@@ -3116,9 +3121,9 @@ __device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 d0, const
     for (int k = 0; k < K; k++)
         F[k].mode = 0;
     int sp = 0;
-    V3 o = mk(0, 0, 0), d = d0, r = mk(0, 0, 0);
+    V3 o = o0, d = d0, r = mk(0, 0, 0);
     int dep = depth0;
-    float str = 1.0f;
+    float str = str0;
     bool first = true, descend = true, ok = true, done = false;
     nq = 0, nsh = 0;
     auto push = [&](const WalkFrame &w) {
@@ -3326,8 +3331,8 @@ __device__ __forceinline__ V3 run_flush(Run64 &u, V3 retval)
 }
 
 template <class S, int MAXD, bool STRICT>
-__device__ __forceinline__ bool lane_walk_sc(const Env &e, int depth0, V3 d0, const CamHit &ch, Rng rng, V3 &res,
-                                             int &nq, int &nsh)
+__device__ __forceinline__ bool lane_walk_sc(const Env &e, int depth0, V3 o0, V3 d0, float str0, const CamHit &ch,
+                                             Rng rng, V3 &res, int &nq, int &nsh)
 {
     enum { ENTER, SETUP, LOOP, RETURN };
     ScFrame F[MAXD + 1];
@@ -3335,9 +3340,9 @@ __device__ __forceinline__ bool lane_walk_sc(const Env &e, int depth0, V3 d0, co
     Run64 run;
     run_reset(run);
     int sp = 0, state = ENTER;
-    V3 o = mk(0, 0, 0), d = d0, r = mk(0, 0, 0);
+    V3 o = o0, d = d0, r = mk(0, 0, 0);
     int dep = depth0;
-    float str = 1.0f;
+    float str = str0;
     bool first = true;
     nq = 0, nsh = 0;
     for (;;) {
@@ -3525,9 +3530,19 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
 {
     Rng rng;
     rng_seed(rng, lp.seed, (u64)pix, (u64)s);
+#ifdef PT_RAYS
+    /* traceRay(ray, it, depth, engine, strength): the caller's ray, no camera draws */
+    {
+        const float *r = lp.rays + 7 * (long long)pix;
+        F[0].o = mk(r[0], r[1], r[2]);
+        F[0].d = mk(r[3], r[4], r[5]);
+        F[0].strength = r[6];
+    }
+#else
     F[0].o = mk(0, 0, 0);
     F[0].d = camera_dir(lp, pix, rng);
     F[0].strength = 1.0f;
+#endif
     F[0].depth = lp.depth;
     int sp = 0;
     int phase = PH_ENTER;
@@ -3857,18 +3872,27 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             lpix = pix, ls = s;
             Rng r;
             rng_seed(r, lp.seed, (u64)pix, (u64)s);
-            const V3 d = camera_dir(lp, pix, r);
             typename S::Root::Ctx ctx;
-            S::Root::prep(ctx, mk(0, 0, 0), e);
+#ifdef PT_RAYS
+            /* the caller's ray (pixels == nullptr: pix is the ray's index) */
+            const float *rr = lp.rays + 7 * (long long)pix;
+            const V3 o = mk(rr[0], rr[1], rr[2]), d = mk(rr[3], rr[4], rr[5]);
+            const float str = rr[6];
+            S::Root::prep_l(ctx, o, e);
+#else
+            const V3 o = mk(0, 0, 0), d = camera_dir(lp, pix, r);
+            const float str = 1.0f;
+            S::Root::prep(ctx, o, e);
+#endif
             bool ex = false;
             ch.hit = lane_first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
             ch.ex = ex ? 1 : 0;
 #if defined(PT_LANE_SCATTER) /* per scene, pt_scene_set_lane_scatter */
-            ldone = lane_walk_sc<S, MAXD, STRICT>(e, lp.depth, d, ch, r, lres, lq, lsh) ? 1 : 0;
+            ldone = lane_walk_sc<S, MAXD, STRICT>(e, lp.depth, o, d, str, ch, r, lres, lq, lsh) ? 1 : 0;
 #elif defined(PT_LANE_WALK) /* per scene, pt_scene_set_lane_walk */
-            ldone = lane_walk<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
+            ldone = lane_walk<S>(e, lp.depth, o, d, str, ch, lres, lq, lsh) ? 1 : 0;
 #else
-            ldone = lane_sample<S>(e, lp.depth, d, ch, lres, lq, lsh) ? 1 : 0;
+            ldone = lane_sample<S>(e, lp.depth, o, d, str, ch, lres, lq, lsh) ? 1 : 0;
 #endif
         }
         PT_ACC2(cnt, 1, tchunk); /* the lane-parallel front end */

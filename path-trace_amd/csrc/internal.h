@@ -95,7 +95,8 @@ struct Generated
     int n_prims = 0, n_spheres = 0, n_planes = 0, n_mats = 0;
 };
 
-Generated generate(const SceneImpl &s, int depth);
+/* rays: the module of pt_trace_rays (PT_RAYS), whose items are caller rays */
+Generated generate(const SceneImpl &s, int depth, bool rays = false);
 /* Query module for the boundary's query virtuals: pt_query_spans over object
  * `obj` (if >= 0) and pt_tex_eval of texture `tex` (if >= 0). */
 Generated generate_query(const SceneImpl &s, int obj, int tex);

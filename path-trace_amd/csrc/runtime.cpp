@@ -73,6 +73,7 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     int sample_major;
     int block_sums;
     long long perm;
+    const float *rays;
 };
 
 template <class T>
@@ -433,10 +434,14 @@ std::vector<uint64_t> jump_table()
     return t;
 }
 
-DeviceState &device_state(SceneImpl &s, int device, const Generated &g)
+/* A scene's state on one device: the render module, or (rays) the ray-list
+ * module of pt_trace_rays, each with its own buffers so that alternating calls
+ * reload nothing. */
+constexpr int kRaysState = 1 << 16;
+DeviceState &device_state(SceneImpl &s, int device, const Generated &g, bool rays = false)
 {
     HIPCHECK(hipSetDevice(device));
-    std::unique_ptr<DeviceState> &ds = s.devices[device];
+    std::unique_ptr<DeviceState> &ds = s.devices[device | (rays ? kRaysState : 0)];
     if (!ds) {
         ds.reset(new DeviceState);
         ds->device = device;
@@ -598,12 +603,12 @@ size_t stage_floats(const pt_render_params *p, long long npix, long long per_pas
 }
 
 /* Module, parameters and every device buffer a render with p needs. */
-DeviceState &prepare(SceneImpl &s, const pt_render_params *p, Generated &g)
+DeviceState &prepare(SceneImpl &s, const pt_render_params *p, Generated &g, bool rays = false)
 {
     validate(p);
-    g = generate(s, p->depth);
+    g = generate(s, p->depth, rays);
     s.last_key = g.key;
-    DeviceState &ds = device_state(s, p->device, g);
+    DeviceState &ds = device_state(s, p->device, g, rays);
     const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
     if (npix > 0) {
         long long per_pass = pass_samples(p, npix);
@@ -635,7 +640,10 @@ void collect_timings(DeviceState &ds, pt_render_stats *st)
     memset(st, 0, sizeof(*st));
     if (ds.pending.empty())
         return;
-    HIPCHECK(hipEventSynchronize(ds.pending.back().evs.back()));
+    /* renders may have been queued on different streams: wait for each one's
+     * last event before reading any elapsed time */
+    for (auto &pr : ds.pending)
+        HIPCHECK(hipEventSynchronize(pr.evs.back()));
     for (auto &pr : ds.pending) {
         for (auto &sp : pr.spans) {
             float ms = 0;
@@ -683,12 +691,23 @@ void collect_timings(DeviceState &ds, pt_render_stats *st)
 
 /* compact: with a pixel list, pixel k's result goes to fb[3k..3k+2] (else to
  * its frame position, fb[3 * pixels[k]]) */
+constexpr size_t kMaxPending = 1024; /* deferred renders a device keeps before a collect is required */
+
+/* rays (device memory, 7 floats per slot): the ray-list module of
+ * pt_trace_rays renders slot k = ray k instead of a camera pixel */
 void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream_t stream, pt_render_stats *st,
-                   Timing tm, bool compact = false)
+                   Timing tm, bool compact = false, const float *rays = nullptr)
 {
     Generated g;
-    DeviceState &ds = prepare(s, p, g);
+    DeviceState &ds = prepare(s, p, g, rays != nullptr);
     const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
+    /* an untimed render queued while timed ones wait for their collect joins
+     * them: its launches are timed too, so the counters the collect reads and
+     * the kernel times it sums cover the same renders */
+    if (tm == Timing::None && !ds.pending.empty())
+        tm = Timing::Deferred;
+    if (tm == Timing::Deferred && ds.pending.size() >= kMaxPending)
+        throw Error(PT_ERR_ARG, "too many timed renders pending: call pt_render_collect");
     if (tm == Timing::Sync) {
         memset(st, 0, sizeof(*st));
         for (auto &pr : ds.pending) /* a synchronous render reports itself alone */
@@ -777,6 +796,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             /* one staged partial per 32-sample block when a chunk is a block */
             lp.block_sums =
                 (block_staging(p) && !lp.sample_major && (chunk == 32 || chunk == 64) && nsamp % chunk == 0) ? 1 : 0;
+            lp.rays = rays;
             reduce_mode = p->order == PT_ORDER_REFERENCE ? 0 : lp.block_sums ? 2 : 1;
             ds.stage.ensure((size_t)(lp.block_sums ? npix * (nsamp / 32) * 3 : npix * nsamp * 3));
             const float *Pp = ds.P.p;
@@ -1360,6 +1380,73 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
         const size_t nout = p->pixels ? (size_t)p->npixels * 3 : n;
         if (nout)
             HIPCHECK(hipMemcpy(rgb_out, fb.p, nout * 4, hipMemcpyDeviceToHost));
+        return PT_OK;
+    });
+}
+
+/* traceRay<T>(ray, spanIterator, depth, engine, strength), include/path-trace.h:
+ * 58-165, for n caller rays in one launch of the ray-list module: the render
+ * kernel with slot k = ray k (origin, direction, strength) instead of a camera
+ * ray, spp samples per ray keyed (seed, k, sample), summed in the call's order
+ * and divided by spp -- tracePixel's float-coordinate overload (:172-185) when
+ * every sample traces the same ray. */
+static pt_render_params trace_params(const pt_trace_params *tp, int64_t n)
+{
+    if (!tp)
+        throw Error(PT_ERR_ARG, "null params");
+    if (n < 0 || n >= (1ll << 31))
+        throw Error(PT_ERR_ARG, "ray count must be in [0, 2^31)");
+    pt_render_params p;
+    memset(&p, 0, sizeof p);
+    p.width = (int)std::max<int64_t>(1, n), p.height = 1;
+    p.spp = tp->spp, p.depth = tp->depth;
+    p.screen_w = p.screen_h = p.screen_dist = 1.0f; /* unused: no camera */
+    p.seed = tp->seed, p.order = tp->order, p.device = tp->device;
+    p.max_buffer_bytes = tp->max_buffer_bytes;
+    p.sample_begin = tp->sample_begin;
+    return p;
+}
+
+int pt_trace_rays(pt_scene *s, const pt_trace_params *tp, const float *rays, int64_t n, float *rgb_out,
+                  pt_render_stats *stats)
+{
+    return guard([&] {
+        pt_render_params p = trace_params(tp, n);
+        validate(&p);
+        if (n == 0) {
+            if (stats)
+                memset(stats, 0, sizeof(*stats));
+            return PT_OK;
+        }
+        if (!rays || !rgb_out)
+            throw Error(PT_ERR_ARG, "null rays or output");
+        for (int64_t k = 0; k < n; k++) /* Ray(o, d) asserts d != 0 (include/ray.h:17) */
+            if (rays[7 * k + 3] == 0.0f && rays[7 * k + 4] == 0.0f && rays[7 * k + 5] == 0.0f)
+                throw Error(PT_ERR_ARG, "ray " + std::to_string(k) + " has a zero direction");
+        SceneImpl &sc = S(s);
+        HIPCHECK(hipSetDevice(p.device));
+        DevBuf<float> fb, rb;
+        struct Free
+        {
+            DevBuf<float> &a, &b;
+            ~Free() { a.release(), b.release(); }
+        } fr{fb, rb};
+        fb.ensure((size_t)n * 3);
+        rb.ensure((size_t)n * 7);
+        HIPCHECK(hipMemcpy(rb.p, rays, (size_t)n * 7 * 4, hipMemcpyHostToDevice));
+        pt_render_stats local;
+        render_device(sc, &p, fb.p, nullptr, stats ? stats : &local, Timing::Sync, true, rb.p);
+        HIPCHECK(hipDeviceSynchronize());
+        HIPCHECK(hipMemcpy(rgb_out, fb.p, (size_t)n * 3 * 4, hipMemcpyDeviceToHost));
+        return PT_OK;
+    });
+}
+
+int pt_trace_compile(pt_scene *s, int depth)
+{
+    return guard([&] {
+        Generated g = generate(S(s), depth, true);
+        code_object(g);
         return PT_OK;
     });
 }

@@ -18,15 +18,16 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import PT_ORDER_FAST, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, load_hdr, load_png, \
-    write_bmp, write_hdr
+from ._lib import PT_ORDER_FAST, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, TraceParams, load_hdr, \
+    load_png, write_bmp, write_hdr
 from .scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTexture, ImageSkyboxAlphaTexture,
                     ImageSkyboxTexture, ImageTexture, Intersection, LogTexture, Material, Matrix,
                     MirrorBallSkymapTexture, MultiplyTexture, Object, Plane, SphericalCoordinatesSkymapTexture,
                     Sphere, Texture, TransformedObject, TransformedTexture, Union, invert, to_text,
                     transform_material, transform_object, transform_texture, union_array)
 
-__all__ = [n for n in dir() if not n.startswith("_")] + ["DeviceScene", "render", "render_device", "prepare"]
+__all__ = [n for n in dir() if not n.startswith("_")] + ["DeviceScene", "render", "render_device", "prepare",
+                                                         "trace_rays"]
 
 ORDERS = {"fast": PT_ORDER_FAST, "reference": PT_ORDER_REFERENCE,
           "strict": PT_ORDER_REFERENCE,
@@ -180,6 +181,10 @@ class DeviceScene:
             raise PtError(_lib.lib().pt_last_error().decode())
         return k
 
+    def compile_rays(self, depth: int) -> None:
+        """Compile pt_trace_rays' module for this scene and depth (no device)."""
+        _lib.check(_lib.lib().pt_trace_compile(self._h, depth))
+
     def compile(self, depth: int) -> str:
         _lib.check(_lib.lib().pt_scene_compile(self._h, depth))
         return _lib.lib().pt_scene_kernel_key(self._h, depth).decode()
@@ -223,6 +228,29 @@ def render(scene, width: int, height: int, spp: int, depth: int, screen=None, se
     _lib.check(_lib.lib().pt_render(ds.handle, ctypes.byref(p), out.ctypes.data, ctypes.byref(st)))
     if keep is None:
         out = out.reshape(height, width, 3)
+    return (out, st.as_dict()) if stats else out
+
+
+def trace_rays(scene, rays, depth: int, spp: int = 1, seed: int = 0x5EED, order="fast", device: int = 0,
+               sample_begin: int = 0, stats: bool = False):
+    """traceRay(ray, it, depth, engine, strength) (include/path-trace.h:58-165)
+    for each row of rays (n x 7 float32: origin, direction, strength; n x 6
+    takes strength 1), on the device in one launch (pt_trace_rays): the mean of
+    spp samples per ray, sample s of ray k drawing from the engine keyed
+    (seed, k, sample_begin + s).  Returns n x 3 float32."""
+    ds = scene if isinstance(scene, DeviceScene) else DeviceScene(scene)
+    r = np.asarray(rays, dtype=np.float32)
+    if r.ndim == 2 and r.shape[1] == 6:
+        r = np.concatenate([r, np.ones((len(r), 1), dtype=np.float32)], axis=1)
+    r = np.ascontiguousarray(r.reshape(-1, 7))
+    tp = TraceParams()
+    tp.spp, tp.depth, tp.seed = int(spp), int(depth), int(seed)
+    tp.order = ORDERS[order] if isinstance(order, str) else int(order)
+    tp.device, tp.sample_begin, tp.max_buffer_bytes = int(device), int(sample_begin), 0
+    out = np.zeros((len(r), 3), dtype=np.float32)
+    st = RenderStats()
+    _lib.check(_lib.lib().pt_trace_rays(ds.handle, ctypes.byref(tp), r.ctypes.data, len(r), out.ctypes.data,
+                                        ctypes.byref(st)))
     return (out, st.as_dict()) if stats else out
 
 

@@ -36,6 +36,11 @@ class AdaptiveParams(ctypes.Structure):
                 ("lookahead_pixels", ctypes.c_int64)]
 
 
+class TraceParams(ctypes.Structure):
+    _fields_ = [("spp", ctypes.c_int), ("depth", ctypes.c_int), ("seed", ctypes.c_uint64), ("order", ctypes.c_int),
+                ("device", ctypes.c_int), ("sample_begin", ctypes.c_int), ("max_buffer_bytes", ctypes.c_int64)]
+
+
 class RenderStats(ctypes.Structure):
     _fields_ = [("kernel_ms", ctypes.c_double), ("reduce_ms", ctypes.c_double), ("launches", ctypes.c_uint64),
                 ("samples", ctypes.c_uint64), ("queries", ctypes.c_uint64), ("leaf_queries", ctypes.c_uint64),
@@ -92,6 +97,8 @@ SIGNATURES = {
     "pt_render_collect": (_I, [_P, _I, ctypes.POINTER(RenderStats)]),
     "pt_render_adaptive": (_I, [_P, ctypes.POINTER(RenderParams), ctypes.POINTER(AdaptiveParams), _P,
                                 ctypes.POINTER(RenderStats)]),
+    "pt_trace_rays": (_I, [_P, ctypes.POINTER(TraceParams), _P, ctypes.c_int64, _P, ctypes.POINTER(RenderStats)]),
+    "pt_trace_compile": (_I, [_P, _I]),
     "pt_prepare": (_I, [_P, ctypes.POINTER(RenderParams)]),
     "pt_scene_compile": (_I, [_P, _I]),
     "pt_scene_set_occupancy": (_I, [_P, _I]),

@@ -1,0 +1,92 @@
+"""traceRay<T>(ray, it, depth, engine, strength) for caller rays (pt_trace_rays,
+include/path-trace.h:58-165): VERDICT r4 missing #3 / next #6.
+
+CPU: the oracle's restatement (oracle_trace_rays) is pinned to the fixtures the
+unmodified reference froze (tests/golden/make_trace_golden.py: ptref
+traceRay<PtSampleEngine> per (ray, sample), reference order), bit for bit.
+GPU: the device's ray-list module against the same fixtures in reference order
+(bit for bit) and against the oracle's fast order (bit for bit), in each lane
+walk mode; strengths below eps, camera-like rays from the origin and rays that
+start inside the CSG solids are part of the fixture rays."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+import pathtrace as pt
+import zoo as T
+from pathtrace.scene import to_text
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = [("p1", "scene_p1"), ("csg", "csg_zoo")]
+
+
+def _golden(name):
+    d = np.load(os.path.join(HERE, "golden", "trace_%s.npz" % name))
+    spp, depth, seed = [int(v) for v in d["meta"]]
+    return d["rays"], d["mean"], spp, depth, seed
+
+
+@pytest.mark.parametrize("name,builder", CASES)
+def test_oracle_trace_rays_matches_reference(built, name, builder, tmp_path):
+    rays, want, spp, depth, seed = _golden(name)
+    txt = to_text(T.build(builder), str(tmp_path))
+    got = O.trace_rays(txt, rays, spp, depth, seed=seed, order=O.ORDER_REFERENCE)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_trace_rays_input_shape():
+    r = T.trace_rays_input(64, seed=3)
+    assert r.shape == (64, 7) and r.dtype == np.float32
+    assert np.all(np.linalg.norm(r[:, 3:6], axis=1) > 0)
+
+
+def test_trace_rays_rejects_zero_direction(built):
+    ds = pt.DeviceScene(T.build("scene_p1"))
+    r = T.trace_rays_input(4, seed=3)
+    r[2, 3:6] = 0.0
+    with pytest.raises(pt.PtError, match="zero direction"):
+        pt.trace_rays(ds, r, depth=4)
+
+
+def test_trace_rays_empty_batch(built):
+    out = pt.trace_rays(pt.DeviceScene(T.build("scene_p1")), np.zeros((0, 7), np.float32), depth=4)
+    assert out.shape == (0, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,builder", CASES)
+def test_gpu_trace_rays_reference_order_bitexact(name, builder):
+    rays, want, spp, depth, seed = _golden(name)
+    got = pt.trace_rays(T.build(builder), rays, depth, spp=spp, seed=seed, order="reference")
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+# scene options of the ray-list module: the spine only, the fast spine, lane walks, lane scatter walks
+MODES = [("csg", "csg_zoo", {}), ("p1", "scene_p1", {"fast_spine": True}), ("p1", "scene_p1", {"lane_walk": 2}),
+         ("csg", "csg_zoo", {"lane_scatter": True})]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,builder,opts", MODES)
+def test_gpu_trace_rays_fast_order_matches_oracle(name, builder, opts, tmp_path):
+    rays, _, _, depth, seed = _golden(name)
+    spp = 3
+    root = T.build(builder)
+    ds = pt.DeviceScene(root, **opts)
+    got = pt.trace_rays(ds, rays, depth, spp=spp, seed=seed, order="fast", sample_begin=5)
+    want = O.trace_rays(to_text(root, str(tmp_path)), rays, spp, depth, seed=seed, sample_begin=5,
+                        order=O.ORDER_FAST)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_trace_rays_block_path(tmp_path):
+    """96 samples per ray: the slot-major launch with 32-sample block partials."""
+    rays, _, _, depth, seed = _golden("p1")
+    rays = rays[::6]
+    root = T.build("scene_p1")
+    got = pt.trace_rays(root, rays, depth, spp=96, seed=seed, order="fast")
+    want = O.trace_rays(to_text(root, str(tmp_path)), rays, 96, depth, seed=seed, order=O.ORDER_FAST)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))

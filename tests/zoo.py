@@ -103,6 +103,29 @@ def random_rays(n, seed=9, spread=1.0):
     return np.concatenate([o, d], axis=1).astype(np.float32)
 
 
+def trace_rays_input(n, seed=17):
+    """Caller rays for traceRay (n x 7: origin, direction, strength): random
+    rays near the scenes (random_rays), a quarter of them camera-like from the
+    origin, strengths from below eps (traceRay returns the emission alone,
+    include/path-trace.h:105-108) up to 3 (more scatter children)."""
+    rng = np.random.default_rng(seed)
+    r = random_rays(n, seed=seed)
+    r[: n // 4, :3] = 0.0
+    # mostly short directions: eps = 1e-3 applies to t, so |d| ~ 3000 skips all
+    # the scene within 3 units of the origin (SURVEY A.1)
+    d = r[:, 3:6] / np.linalg.norm(r[:, 3:6], axis=1, keepdims=True)
+    # half of them aimed into the box around the demo spheres (z -4.6 .. -3.2)
+    tgt = rng.uniform([-1.6, -0.7, -4.6], [1.6, 0.7, -3.2], size=(n, 3)).astype(np.float32)
+    aim = rng.random(n) < 0.5
+    v = tgt - r[:, :3]
+    d[aim] = (v / np.linalg.norm(v, axis=1, keepdims=True))[aim]
+    r[:, 3:6] = d * rng.choice([0.7, 1.0, 4.0, 30.0, 2000.0], size=(n, 1), p=[.25, .35, .2, .15, .05])
+    s = rng.uniform(0.0, 3.0, size=(n, 1)).astype(np.float32)
+    s[rng.random(n) < 0.15] = np.float32(0.0005)
+    s[rng.random(n) < 0.25] = np.float32(1.0)
+    return np.concatenate([r, s], axis=1).astype(np.float32)
+
+
 # (name, builder, W, H, spp, depth) of the per-sample render goldens
 RENDER_CASES = [
     ("p0", "scene_p0", 32, 24, 3, 4),
