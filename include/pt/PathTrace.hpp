@@ -32,9 +32,15 @@
 #ifndef PT_PATHTRACE_HPP
 #define PT_PATHTRACE_HPP
 
+#include <algorithm>
 #include <cctype>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <exception>
 #include <map>
+#include <mutex>
+#include <thread>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -703,6 +709,19 @@ public:
         p.pixels = pixels, p.npixels = npixels;
         ptCheck(pt_render(q_->s, &p, rgb, nullptr));
     }
+    /* traceRay's device side: n rays of 7 floats (origin, direction, strength),
+     * spp samples each, engine keys ray_begin + k (pt_trace_rays) */
+    void renderRays(const float *rays, int64_t n, int spp, int depth, uint64_t seed, int order, int64_t ray_begin,
+                    float *rgb) const
+    {
+        if (!root_set_) {
+            ptCheck(pt_set_root(q_->s, q_->id));
+            root_set_ = true;
+        }
+        pt_trace_params p = {};
+        p.spp = spp, p.depth = depth, p.seed = seed, p.order = order, p.ray_begin = ray_begin;
+        ptCheck(pt_trace_rays(q_->s, &p, rays, n, rgb, nullptr));
+    }
     const Span &operator*() const override { return spans_.at(k_); }
     const Span *operator->() const override { return &spans_.at(k_); }
     bool isAtEnd() const override { return k_ >= spans_.size(); }
@@ -756,6 +775,11 @@ struct FrameEngine
 {
     uint64_t seed;
     int order;
+    /* traceRay / float-coordinate tracePixel calls key their samples by a ray
+     * index: the next one this engine hands out (successive calls draw fresh
+     * streams, as successive calls of the reference draw on from its engine;
+     * not thread-safe, like the reference's engines) */
+    uint64_t rays = 0;
     explicit FrameEngine(uint64_t seed = 0x5EED, int order = PT_ORDER_FAST) : seed(seed), order(order) {}
 };
 
@@ -867,6 +891,195 @@ inline Color tracePixel(SpanIterator &spanIterator, int px, int py, int screenXR
     return tracePixel(spanIterator, px, py, screenXResolution, screenYResolution, sampleCount, rayDepth, screenWidth,
                       screenHeight, screenDistance, defaultFrameEngine());
 }
+
+static inline DeviceSpanIterator &deviceIterator(SpanIterator &spanIterator, const char *who)
+{
+    DeviceSpanIterator *it = dynamic_cast<DeviceSpanIterator *>(&spanIterator);
+    if (!it)
+        throw DeviceError(PT_ERR_ARG, std::string(who) + ": needs the span iterator of a built-in object "
+                                                          "(Object::makeSpanIterator)");
+    return *it;
+}
+
+/* traceRay<T>(ray, spanIterator, depth, engine, strength) of include/path-
+ * trace.h:58-165 over a batch, in one device launch: colors[k] = the mean of
+ * `samples` traceRay values of rays[k] with strengths[k] (nullptr: 1), sample
+ * s of ray k drawing from the engine keyed (engine.seed, engine.rays + k, s);
+ * the engine then hands out the next n keys. */
+inline void traceRays(SpanIterator &spanIterator, const Ray *rays, const float *strengths, size_t n, Color *colors,
+                      int rayDepth, FrameEngine &engine, int samples = 1)
+{
+    DeviceSpanIterator &it = deviceIterator(spanIterator, "traceRay");
+    if (n == 0)
+        return;
+    std::vector<float> r(7 * n);
+    for (size_t k = 0; k < n; k++) {
+        const float v[7] = {rays[k].origin.x, rays[k].origin.y, rays[k].origin.z, rays[k].dir.x,
+                            rays[k].dir.y,    rays[k].dir.z,    strengths ? strengths[k] : 1.0f};
+        std::copy(v, v + 7, &r[7 * k]);
+    }
+    static_assert(sizeof(Color) == 3 * sizeof(float), "Color must be 3 packed floats");
+    it.renderRays(r.data(), (int64_t)n, samples, rayDepth, engine.seed, engine.order, (int64_t)engine.rays,
+                  reinterpret_cast<float *>(colors));
+    engine.rays += n;
+}
+
+/* traceRay with a FrameEngine: one ray, the engine's next key */
+inline Color traceRay(const Ray &ray, SpanIterator &spanIterator, int depth, FrameEngine &randomEngine,
+                      float strength = 1.0f)
+{
+    Color c;
+    traceRays(spanIterator, &ray, &strength, 1, &c, depth, randomEngine);
+    return c;
+}
+
+/* traceRay with any other engine type T (unsigned operator()(), include/
+ * vector3d.h:14-34): two of its draws make the run seed of this call */
+template <typename T>
+inline Color traceRay(const Ray &ray, SpanIterator &spanIterator, int depth, T &randomEngine, float strength = 1.0f)
+{
+    const uint64_t hi = (uint32_t)randomEngine(), lo = (uint32_t)randomEngine();
+    FrameEngine e((hi << 32) | lo);
+    return traceRay(ray, spanIterator, depth, e, strength);
+}
+
+/* traceRay(ray, spanIterator[, depth]) with the global engine (path-trace.h:59's defaults) */
+inline Color traceRay(const Ray &ray, SpanIterator &spanIterator, int depth = DefaultRayDepth)
+{
+    return traceRay(ray, spanIterator, depth, defaultFrameEngine(), 1.0f);
+}
+
+/* tracePixel's float-coordinate overload (include/path-trace.h:172-185): the
+ * ray through (px, py) -- no jitter, computed in float as the reference does --
+ * traced sampleCount times and averaged, in one device launch. */
+inline Color tracePixel(SpanIterator &spanIterator, float px, float py, float screenXResolution,
+                        float screenYResolution, int sampleCount, int rayDepth, float screenWidth, float screenHeight,
+                        float screenDistance, FrameEngine &randomEngine)
+{
+    const float x = 2 * px / screenXResolution - 1;
+    const float y = 1 - 2 * py / screenYResolution;
+    const Ray ray(Vector3D(0, 0, 0), Vector3D(x * screenWidth, y * screenHeight, -screenDistance));
+    const float strength = 1.0f;
+    Color c;
+    traceRays(spanIterator, &ray, &strength, 1, &c, rayDepth, randomEngine, sampleCount);
+    return c;
+}
+template <typename T>
+inline Color tracePixel(SpanIterator &spanIterator, float px, float py, float screenXResolution,
+                        float screenYResolution, int sampleCount, int rayDepth, float screenWidth, float screenHeight,
+                        float screenDistance, T &randomEngine)
+{
+    const uint64_t hi = (uint32_t)randomEngine(), lo = (uint32_t)randomEngine();
+    FrameEngine e((hi << 32) | lo);
+    return tracePixel(spanIterator, px, py, screenXResolution, screenYResolution, sampleCount, rayDepth, screenWidth,
+                      screenHeight, screenDistance, e);
+}
+
+/* Coalesces the per-pixel tracePixel calls of many host threads into device
+ * batches: the shape of the reference demo's RenderBlock pool, whose threads
+ * each call tracePixel for one pixel at a time (src/test.cpp:441-465, the call
+ * at :450; one thread per core, :204).  tracePixel() is thread-safe and blocks
+ * until its pixel's batch is traced; a batch launches when maxBatch calls wait
+ * or maxWaitUs after its first call.  Pixels keep the bits tracePixels gives
+ * them alone (keys depend on the pixel only). */
+class PixelBatcher
+{
+public:
+    PixelBatcher(SpanIterator &spanIterator, int screenXResolution, int screenYResolution, int sampleCount,
+                 int rayDepth, float screenWidth, float screenHeight, float screenDistance,
+                 const FrameEngine &engine = FrameEngine(), size_t maxBatch = 4096, int maxWaitUs = 200)
+        : it_(spanIterator), W_(screenXResolution), H_(screenYResolution), spp_(sampleCount), depth_(rayDepth),
+          sw_(screenWidth), sh_(screenHeight), dist_(screenDistance), engine_(engine),
+          maxBatch_(maxBatch ? maxBatch : 1), maxWaitUs_(maxWaitUs), worker_([this] { run(); })
+    {
+    }
+    ~PixelBatcher()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        worker_.join();
+    }
+    PixelBatcher(const PixelBatcher &) = delete;
+    PixelBatcher &operator=(const PixelBatcher &) = delete;
+
+    Color tracePixel(int px, int py)
+    {
+        Req r;
+        r.x = px, r.y = py;
+        std::unique_lock<std::mutex> lk(m_);
+        if (stop_)
+            throw std::logic_error("PixelBatcher: stopped");
+        queue_.push_back(&r);
+        cv_.notify_all();
+        done_.wait(lk, [&] { return r.done; });
+        if (r.err)
+            std::rethrow_exception(r.err);
+        return r.c;
+    }
+    uint64_t launches() const
+    {
+        std::lock_guard<std::mutex> g(m_);
+        return launches_;
+    }
+    uint64_t pixels() const
+    {
+        std::lock_guard<std::mutex> g(m_);
+        return pixels_;
+    }
+
+private:
+    struct Req
+    {
+        int x = 0, y = 0;
+        Color c;
+        bool done = false;
+        std::exception_ptr err;
+    };
+    void run()
+    {
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+            if (queue_.empty() && stop_)
+                return;
+            cv_.wait_for(lk, std::chrono::microseconds(maxWaitUs_),
+                         [&] { return stop_ || queue_.size() >= maxBatch_; });
+            const size_t n = std::min(queue_.size(), maxBatch_);
+            std::vector<Req *> batch(queue_.begin(), queue_.begin() + (std::ptrdiff_t)n);
+            queue_.erase(queue_.begin(), queue_.begin() + (std::ptrdiff_t)n);
+            lk.unlock();
+            std::vector<int32_t> xs(n), ys(n);
+            std::vector<Color> cs(n);
+            std::exception_ptr err;
+            for (size_t k = 0; k < n; k++) xs[k] = batch[k]->x, ys[k] = batch[k]->y;
+            try {
+                tracePixels(it_, xs.data(), ys.data(), n, cs.data(), W_, H_, spp_, depth_, sw_, sh_, dist_, engine_);
+            } catch (...) {
+                err = std::current_exception();
+            }
+            lk.lock();
+            for (size_t k = 0; k < n; k++) batch[k]->c = cs[k], batch[k]->err = err, batch[k]->done = true;
+            launches_++;
+            pixels_ += n;
+            done_.notify_all();
+        }
+    }
+    SpanIterator &it_;
+    const int W_, H_, spp_, depth_;
+    const float sw_, sh_, dist_;
+    const FrameEngine engine_;
+    const size_t maxBatch_;
+    const int maxWaitUs_;
+    mutable std::mutex m_;
+    std::condition_variable cv_, done_;
+    std::vector<Req *> queue_;
+    bool stop_ = false;
+    uint64_t launches_ = 0, pixels_ = 0;
+    std::thread worker_; /* last: started once every member above is constructed */
+};
 
 class TransformedObject : public Object /* object.h:26-98 */
 {

@@ -210,7 +210,7 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
  * device launch.  rays = n records of 7 floats: origin xyz, direction xyz
  * (non-zero: Ray's assert, include/ray.h:17; not normalised), strength.
  * rgb_out receives, per ray, the mean of spp traceRay samples -- sample s of ray
- * k drawing from the engine keyed (seed, k, sample_begin + s), include/pt/
+ * k drawing from the engine keyed (seed, ray_begin + k, sample_begin + s), include/pt/
  * pt_engine.h -- summed in `order` and divided by spp: with spp = 1 the
  * traceRay value itself (as (0 + c) / 1: a -0 channel reads +0), with the
  * camera ray of a point and spp = sampleCount tracePixel's float-coordinate
@@ -223,6 +223,8 @@ typedef struct pt_trace_params {
     int device;                    /* HIP device ordinal                                        */
     int sample_begin;              /* engine sample index of the first sample                   */
     int64_t max_buffer_bytes;      /* per-sample staging budget (0 = 8 GiB)                     */
+    int64_t ray_begin;             /* engine key index of rays[0] (ray k: ray_begin + k), so
+                                      successive calls can draw fresh streams                  */
 } pt_trace_params;
 int pt_trace_rays(pt_scene *s, const pt_trace_params *p, const float *rays, int64_t n, float *rgb_out,
                   pt_render_stats *stats);

@@ -1296,10 +1296,10 @@ int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int 
 /* traceRay<T>(ray, it, depth, engine, strength), include/path-trace.h:58-165,
  * for n caller rays (7 floats: origin, direction, strength): per ray the sum of
  * spp samples in `order` (pixel_sum), sample s drawing from the engine keyed
- * (seed, ray index, sample_begin + s), each sample (0 + c) / 1 as a one-sample
+ * (seed, ray_begin + ray index, sample_begin + s), each sample (0 + c) / 1 as a one-sample
  * tracePixel adds it, divided by spp -- what pt_trace_rays computes. */
 int oracle_trace_rays(const char *scene_text, const float *rays, int n, int spp, int depth, uint64_t seed,
-                      int sample_begin, int threads, int order, float *out)
+                      int sample_begin, int64_t ray_begin, int threads, int order, float *out)
 {
     try {
         std::unique_ptr<Scene> scene = load_scene(scene_text);
@@ -1316,7 +1316,7 @@ int oracle_trace_rays(const char *scene_text, const float *rays, int n, int spp,
                     const float *r = rays + 7 * (size_t)k;
                     const Ray ray{V3(r[0], r[1], r[2]), V3(r[3], r[4], r[5])};
                     V3 acc = pixel_sum(spp, order == 1 ? ORDER_FAST : ORDER_REFERENCE, [&](int s) {
-                        SampleEngine e(seed, (uint64_t)k, (uint64_t)(sample_begin + s));
+                        SampleEngine e(seed, (uint64_t)(ray_begin + k), (uint64_t)(sample_begin + s));
                         V3 c = V3(0, 0, 0) + tr.trace(ray, depth, e, r[6]);
                         return c / (float)1;
                     });

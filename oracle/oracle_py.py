@@ -64,7 +64,7 @@ def lib():
                                              C.c_void_p, C.c_void_p]
         L.oracle_trace_rays.restype = C.c_int
         L.oracle_trace_rays.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int,
-                                        C.c_int, C.c_int, C.c_void_p]
+                                        C.c_int64, C.c_int, C.c_int, C.c_void_p]
         L.oracle_kat.restype = ctypes.c_int
         L.oracle_kat.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         _lib = L
@@ -124,13 +124,13 @@ def render_adaptive(scene_text: str, W: int, H: int, spp: int, depth: int, block
 
 
 def trace_rays(scene_text: str, rays: np.ndarray, spp: int, depth: int, seed: int = 0x5EED, sample_begin: int = 0,
-               threads: int = 0, order: int = ORDER_REFERENCE):
+               threads: int = 0, order: int = ORDER_REFERENCE, ray_begin: int = 0):
     """traceRay per caller ray (n x 7: origin, direction, strength): the mean
     of spp samples keyed (seed, ray, sample) -- pt_trace_rays' restatement."""
     r = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 7)
     out = np.zeros((len(r), 3), dtype=np.float32)
     rc = lib().oracle_trace_rays(scene_text.encode(), r.ctypes.data, len(r), spp, depth, seed, sample_begin,
-                                 threads or (os.cpu_count() or 1), order, out.ctypes.data)
+                                 ray_begin, threads or (os.cpu_count() or 1), order, out.ctypes.data)
     if rc != 0:
         raise RuntimeError("oracle_trace_rays: " + lib().oracle_last_error().decode())
     return out

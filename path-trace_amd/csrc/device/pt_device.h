@@ -81,7 +81,15 @@ struct PtLaunch
     const float *rays;  /* PT_RAYS modules (pt_trace_rays): slot k's ray, 7 floats
                            (origin, direction, strength) -- traceRay's arguments,
                            include/path-trace.h:59 -- instead of a camera ray    */
+    long long ray0;     /* PT_RAYS: engine key index of slot 0 (slot k: ray0 + k) */
 };
+/* The engine key index of a slot's item: its pixel index, or in a ray-list
+ * module the caller's ray index */
+#ifdef PT_RAYS
+#define PT_ITEM_KEY(lp, pix) ((u64)((lp).ray0 + (long long)(pix)))
+#else
+#define PT_ITEM_KEY(lp, pix) ((u64)(pix))
+#endif
 
 struct Env
 {
@@ -3529,7 +3537,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                                            const CamHit &cam)
 {
     Rng rng;
-    rng_seed(rng, lp.seed, (u64)pix, (u64)s);
+    rng_seed(rng, lp.seed, PT_ITEM_KEY(lp, pix), (u64)s);
 #ifdef PT_RAYS
     /* traceRay(ray, it, depth, engine, strength): the caller's ray, no camera draws */
     {
@@ -3871,7 +3879,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             const int pix = pixels ? pixels[slot] : (int)slot;
             lpix = pix, ls = s;
             Rng r;
-            rng_seed(r, lp.seed, (u64)pix, (u64)s);
+            rng_seed(r, lp.seed, PT_ITEM_KEY(lp, pix), (u64)s);
             typename S::Root::Ctx ctx;
 #ifdef PT_RAYS
             /* the caller's ray (pixels == nullptr: pix is the ray's index) */

@@ -74,6 +74,7 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     int block_sums;
     long long perm;
     const float *rays;
+    long long ray0;
 };
 
 template <class T>
@@ -696,7 +697,7 @@ constexpr size_t kMaxPending = 1024; /* deferred renders a device keeps before a
 /* rays (device memory, 7 floats per slot): the ray-list module of
  * pt_trace_rays renders slot k = ray k instead of a camera pixel */
 void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream_t stream, pt_render_stats *st,
-                   Timing tm, bool compact = false, const float *rays = nullptr)
+                   Timing tm, bool compact = false, const float *rays = nullptr, int64_t ray0 = 0)
 {
     Generated g;
     DeviceState &ds = prepare(s, p, g, rays != nullptr);
@@ -797,6 +798,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             lp.block_sums =
                 (block_staging(p) && !lp.sample_major && (chunk == 32 || chunk == 64) && nsamp % chunk == 0) ? 1 : 0;
             lp.rays = rays;
+            lp.ray0 = ray0;
             reduce_mode = p->order == PT_ORDER_REFERENCE ? 0 : lp.block_sums ? 2 : 1;
             ds.stage.ensure((size_t)(lp.block_sums ? npix * (nsamp / 32) * 3 : npix * nsamp * 3));
             const float *Pp = ds.P.p;
@@ -1396,6 +1398,8 @@ static pt_render_params trace_params(const pt_trace_params *tp, int64_t n)
         throw Error(PT_ERR_ARG, "null params");
     if (n < 0 || n >= (1ll << 31))
         throw Error(PT_ERR_ARG, "ray count must be in [0, 2^31)");
+    if (tp->ray_begin < 0 || tp->ray_begin + n > (1ll << 43))
+        throw Error(PT_ERR_ARG, "ray keys must lie in [0, 2^43) (engine key layout)");
     pt_render_params p;
     memset(&p, 0, sizeof p);
     p.width = (int)std::max<int64_t>(1, n), p.height = 1;
@@ -1435,7 +1439,7 @@ int pt_trace_rays(pt_scene *s, const pt_trace_params *tp, const float *rays, int
         rb.ensure((size_t)n * 7);
         HIPCHECK(hipMemcpy(rb.p, rays, (size_t)n * 7 * 4, hipMemcpyHostToDevice));
         pt_render_stats local;
-        render_device(sc, &p, fb.p, nullptr, stats ? stats : &local, Timing::Sync, true, rb.p);
+        render_device(sc, &p, fb.p, nullptr, stats ? stats : &local, Timing::Sync, true, rb.p, tp->ray_begin);
         HIPCHECK(hipDeviceSynchronize());
         HIPCHECK(hipMemcpy(rgb_out, fb.p, (size_t)n * 3 * 4, hipMemcpyDeviceToHost));
         return PT_OK;

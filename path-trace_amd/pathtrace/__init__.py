@@ -232,12 +232,12 @@ def render(scene, width: int, height: int, spp: int, depth: int, screen=None, se
 
 
 def trace_rays(scene, rays, depth: int, spp: int = 1, seed: int = 0x5EED, order="fast", device: int = 0,
-               sample_begin: int = 0, stats: bool = False):
+               sample_begin: int = 0, ray_begin: int = 0, stats: bool = False):
     """traceRay(ray, it, depth, engine, strength) (include/path-trace.h:58-165)
     for each row of rays (n x 7 float32: origin, direction, strength; n x 6
     takes strength 1), on the device in one launch (pt_trace_rays): the mean of
     spp samples per ray, sample s of ray k drawing from the engine keyed
-    (seed, k, sample_begin + s).  Returns n x 3 float32."""
+    (seed, ray_begin + k, sample_begin + s).  Returns n x 3 float32."""
     ds = scene if isinstance(scene, DeviceScene) else DeviceScene(scene)
     r = np.asarray(rays, dtype=np.float32)
     if r.ndim == 2 and r.shape[1] == 6:
@@ -246,7 +246,7 @@ def trace_rays(scene, rays, depth: int, spp: int = 1, seed: int = 0x5EED, order=
     tp = TraceParams()
     tp.spp, tp.depth, tp.seed = int(spp), int(depth), int(seed)
     tp.order = ORDERS[order] if isinstance(order, str) else int(order)
-    tp.device, tp.sample_begin, tp.max_buffer_bytes = int(device), int(sample_begin), 0
+    tp.device, tp.sample_begin, tp.max_buffer_bytes, tp.ray_begin = int(device), int(sample_begin), 0, int(ray_begin)
     out = np.zeros((len(r), 3), dtype=np.float32)
     st = RenderStats()
     _lib.check(_lib.lib().pt_trace_rays(ds.handle, ctypes.byref(tp), r.ctypes.data, len(r), out.ctypes.data,

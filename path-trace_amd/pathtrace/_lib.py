@@ -38,7 +38,8 @@ class AdaptiveParams(ctypes.Structure):
 
 class TraceParams(ctypes.Structure):
     _fields_ = [("spp", ctypes.c_int), ("depth", ctypes.c_int), ("seed", ctypes.c_uint64), ("order", ctypes.c_int),
-                ("device", ctypes.c_int), ("sample_begin", ctypes.c_int), ("max_buffer_bytes", ctypes.c_int64)]
+                ("device", ctypes.c_int), ("sample_begin", ctypes.c_int), ("max_buffer_bytes", ctypes.c_int64),
+                ("ray_begin", ctypes.c_int64)]
 
 
 class RenderStats(ctypes.Structure):

@@ -9,11 +9,16 @@
 //                                          t0 n0 m0 t1 n1 m1 (m = material index below)
 //   facade_p1 tex HDR PTS OUT           -> getColor / getFloat of MirrorBall(Image(HDR))
 //                                          and of a user-defined Texture at each point
+//   facade_p1 traceray RAYS DEPTH SPP OUT  -> traceRay for n x 7 caller rays (reference order)
+//   facade_p1 latency W H SPP DEPTH THREADS OUT.json -> per-call tracePixel latency,
+//                                          one-batch and PixelBatcher throughput
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <chrono>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "pt/PathTrace.hpp"
@@ -182,6 +187,114 @@ int main(int argc, char **argv)
             if (!f)
                 return 5;
             fwrite(img.data(), sizeof(Color), img.size(), f);
+            fclose(f);
+            return 0;
+        }
+        if (!strcmp(argv[1], "traceray") && argc == 6) {
+            /* traceRay for caller rays (RAYS: n x 7 floats) in reference order:
+             * the batch with `spp` samples per ray goes to OUT; per-call traceRay,
+             * the T-engine overload and the float-coordinate tracePixel are
+             * checked against batches with the same keys */
+            std::vector<float> rv = read_f32(argv[2]);
+            const int depth = atoi(argv[3]), spp = atoi(argv[4]);
+            const size_t n = rv.size() / 7;
+            std::vector<Ray> rays;
+            std::vector<float> str;
+            for (size_t k = 0; k < n; k++) {
+                const float *q = &rv[7 * k];
+                rays.push_back(Ray(Vector3D(q[0], q[1], q[2]), Vector3D(q[3], q[4], q[5])));
+                str.push_back(q[6]);
+            }
+            std::unique_ptr<SpanIterator> it(world->makeSpanIterator());
+            std::vector<Color> batch(n), one(n), calls(n);
+            FrameEngine eb(0x5EED, PT_ORDER_REFERENCE);
+            traceRays(*it, rays.data(), str.data(), n, batch.data(), depth, eb, spp);
+            if (eb.rays != n)
+                return 10;
+            FrameEngine e1(0x5EED, PT_ORDER_REFERENCE), e2(0x5EED, PT_ORDER_REFERENCE);
+            traceRays(*it, rays.data(), str.data(), n, one.data(), depth, e1);
+            for (size_t k = 0; k < n && k < 24; k++) /* the per-call overload: the engine's next key */
+                if (memcmp(&one[k], &(calls[k] = traceRay(rays[k], *it, depth, e2, str[k])), sizeof(Color)))
+                    return 11;
+            struct Lcg /* a reference-style engine type (include/vector3d.h:14-34) */
+            {
+                uint64_t v = 0x12476242;
+                static unsigned min() { return 0; }
+                static unsigned max() { return 0xFFFFFFFF; }
+                unsigned operator()() { return (unsigned)((v = 214013 * v + 2531011) >> 32); }
+            } lcg;
+            Color t = traceRay(rays[0], *it, depth, lcg, 1.0f);
+            Color p = tracePixel(*it, 10.5f, 7.25f, 40.0f, 30.0f, 3, depth, 40.0f, 30.0f, 60.0f, lcg);
+            if (!(t.x == t.x) || !(p.x == p.x))
+                return 12;
+            /* float tracePixel == the batch of its camera ray (same keys) */
+            FrameEngine e3, e4;
+            Color fp = tracePixel(*it, 10.5f, 7.25f, 40.0f, 30.0f, 3, depth, 40.0f, 30.0f, 60.0f, e3);
+            const float x = 2 * 10.5f / 40.0f - 1, y = 1 - 2 * 7.25f / 30.0f;
+            Ray cam(Vector3D(0, 0, 0), Vector3D(x * 40.0f, y * 30.0f, -60.0f));
+            Color fb;
+            traceRays(*it, &cam, nullptr, 1, &fb, depth, e4, 3);
+            if (memcmp(&fp, &fb, sizeof(Color)))
+                return 13;
+            FILE *f = fopen(argv[5], "wb");
+            if (!f)
+                return 5;
+            fwrite(batch.data(), sizeof(Color), n, f);
+            fclose(f);
+            return 0;
+        }
+        if (!strcmp(argv[1], "latency") && argc == 8) {
+            /* the demo's per-pixel call shape against the device: per-call
+             * tracePixel latency, one batch for the frame, and the PixelBatcher
+             * under THREADS host threads each calling tracePixel pixel by pixel */
+            const int W = atoi(argv[2]), H = atoi(argv[3]), spp = atoi(argv[4]), depth = atoi(argv[5]);
+            const int threads = atoi(argv[6]);
+            const float sw = (float)W, sh = (float)H, dist = (float)(2 * (W < H ? W : H));
+            std::unique_ptr<SpanIterator> it(world->makeSpanIterator());
+            FrameEngine eng;
+            using clk = std::chrono::steady_clock;
+            auto secs = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
+            tracePixel(*it, 0, 0, W, H, spp, depth, sw, sh, dist, eng); /* compile / load / allocate */
+            const int ncall = W * H < 256 ? W * H : 256;
+            clk::time_point t0 = clk::now();
+            for (int k = 0; k < ncall; k++)
+                tracePixel(*it, k % W, k / W, W, H, spp, depth, sw, sh, dist, eng);
+            const double per_call = secs(t0) / ncall;
+            std::vector<int32_t> xs, ys;
+            for (int y = 0; y < H; y++)
+                for (int x = 0; x < W; x++) xs.push_back(x), ys.push_back(y);
+            std::vector<Color> frame(xs.size()), viaq(xs.size());
+            t0 = clk::now();
+            tracePixels(*it, xs.data(), ys.data(), xs.size(), frame.data(), W, H, spp, depth, sw, sh, dist, eng);
+            const double batch = secs(t0);
+            uint64_t launches = 0;
+            double pooled = 0;
+            {
+                PixelBatcher q(*it, W, H, spp, depth, sw, sh, dist, eng, 4096, 200);
+                t0 = clk::now();
+                std::vector<std::thread> pool;
+                for (int t = 0; t < threads; t++)
+                    pool.emplace_back([&, t] {
+                        for (int y = t; y < H; y += threads)
+                            for (int x = 0; x < W; x++) viaq[(size_t)y * W + x] = q.tracePixel(x, y);
+                    });
+                for (auto &th : pool) th.join();
+                pooled = secs(t0);
+                launches = q.launches();
+            }
+            if (memcmp(frame.data(), viaq.data(), frame.size() * sizeof(Color)))
+                return 14;
+            FILE *f = fopen(argv[7], "w");
+            if (!f)
+                return 5;
+            fprintf(f,
+                    "{\"W\": %d, \"H\": %d, \"spp\": %d, \"depth\": %d, \"threads\": %d, "
+                    "\"per_call_us\": %.1f, \"per_call_calls\": %d, \"batch_s\": %.6f, \"batch_us_per_pixel\": %.3f, "
+                    "\"batcher_s\": %.6f, \"batcher_launches\": %llu, \"batcher_mean_batch\": %.1f, "
+                    "\"batcher_us_per_pixel\": %.3f}\n",
+                    W, H, spp, depth, threads, per_call * 1e6, ncall, batch, batch * 1e6 / (W * H), pooled,
+                    (unsigned long long)launches, (double)(W * H) / (double)(launches ? launches : 1),
+                    pooled * 1e6 / (W * H));
             fclose(f);
             return 0;
         }

@@ -19,7 +19,7 @@ LIBDIR = os.path.join(ROOT, "path-trace_amd", "lib")
 @pytest.fixture(scope="module")
 def facade_bin(built, tmp_path_factory):
     out = str(tmp_path_factory.mktemp("facade") / "facade_p1")
-    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Wextra", "-Werror",
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Wextra", "-Werror", "-pthread",
                     "-I" + os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "cpp", "facade_p1.cpp"),
                     "-L" + LIBDIR, "-lpt", "-Wl,-rpath," + LIBDIR, "-o", out], check=True)
     return out
@@ -120,3 +120,36 @@ def test_facade_texture_virtuals(facade_bin, tmp_path):
     chk = np.where((np.floor(pts).astype(np.int64).sum(axis=1) % 2) != 0, 1.0, 0.25).astype(np.float32)
     np.testing.assert_array_equal(got[:, 4], chk)
     np.testing.assert_array_equal(got[:, 7], ((chk + chk) + chk) * np.float32(1.0 / 3.0))
+
+
+@pytest.mark.gpu
+def test_facade_trace_ray_bitexact(facade_bin, tmp_path):
+    """traceRay<T> / traceRays through the facade (pt_trace_rays): the fixture
+    rays in reference order give the unmodified reference's traceRay means bit
+    for bit (tests/golden/trace_p1.npz); the binary itself checks the per-call
+    overload, the T-engine overload and the float-coordinate tracePixel against
+    batches with the same engine keys (exit codes 10-13)."""
+    d = np.load(os.path.join(ROOT, "tests", "golden", "trace_p1.npz"))
+    spp, depth, _ = [int(v) for v in d["meta"]]
+    rp, out = str(tmp_path / "rays.bin"), str(tmp_path / "tr.bin")
+    d["rays"].astype(np.float32).tofile(rp)
+    r = subprocess.run([facade_bin, "traceray", rp, str(depth), str(spp), out], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, (r.returncode, r.stderr)
+    got = np.fromfile(out, dtype=np.float32).reshape(-1, 3)
+    np.testing.assert_array_equal(got.view(np.uint32), d["mean"].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_facade_pixel_batcher(facade_bin, tmp_path):
+    """The demo's per-pixel call shape from 8 host threads through PixelBatcher:
+    the same bits as one batch for the frame (exit code 14 otherwise), in far
+    fewer launches than pixels; per-call latency recorded."""
+    import json
+    out = str(tmp_path / "lat.json")
+    r = subprocess.run([facade_bin, "latency", "48", "32", "4", "8", "8", out], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, (r.returncode, r.stderr)
+    d = json.load(open(out))
+    assert d["per_call_us"] > 0 and d["batcher_launches"] >= 1
+    assert d["batcher_launches"] < 48 * 32 / 2

@@ -75,9 +75,9 @@ def test_gpu_trace_rays_fast_order_matches_oracle(name, builder, opts, tmp_path)
     spp = 3
     root = T.build(builder)
     ds = pt.DeviceScene(root, **opts)
-    got = pt.trace_rays(ds, rays, depth, spp=spp, seed=seed, order="fast", sample_begin=5)
+    got = pt.trace_rays(ds, rays, depth, spp=spp, seed=seed, order="fast", sample_begin=5, ray_begin=1000)
     want = O.trace_rays(to_text(root, str(tmp_path)), rays, spp, depth, seed=seed, sample_begin=5,
-                        order=O.ORDER_FAST)
+                        order=O.ORDER_FAST, ray_begin=1000)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
