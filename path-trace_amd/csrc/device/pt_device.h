@@ -2103,6 +2103,9 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 #ifndef PT_LANE_MAJOR
 #define PT_LANE_MAJOR 1 /* deferred rounds: lane l evaluates attempts 8l..8l+7 (one chained stream) */
 #endif
+#ifndef PT_LM_CHAINS
+#define PT_LM_CHAINS 1 /* lane-major rounds: engine chains per lane (2: the halves interleaved) */
+#endif
 
 #ifndef PT_PASS_PAIR_FALLBACK
 /* 0: in a burst's fast pass over a Difference-free tree, lanes the one-pass
@@ -2252,6 +2255,18 @@ __device__ __forceinline__ Attempt2 attempt2_chain(u64 &s, V3 n, V3 kR)
     const W2 a1 = lcg_step({(u32)s, (u32)(s >> 32)}), a2 = lcg_step(a1), a3 = lcg_step(a2);
     const W2 b1 = lcg_step(a3), b2 = lcg_step(b1), b3 = lcg_step(b2);
     s = ((u64)b3.hi << 32) | (u64)b3.lo;
+    return attempt2_draws<KR0>(a1, a2, a3, b1, b2, b3, n, kR);
+}
+/* Two attempts from two independent streams (sa, sb), each advanced past its
+ * attempt's three draws: the two engine chains interleave. */
+template <bool KR0>
+__device__ __forceinline__ Attempt2 attempt2_split(u64 &sa, u64 &sb, V3 n, V3 kR)
+{
+    const W2 a1 = lcg_step({(u32)sa, (u32)(sa >> 32)}), b1 = lcg_step({(u32)sb, (u32)(sb >> 32)});
+    const W2 a2 = lcg_step(a1), b2 = lcg_step(b1);
+    const W2 a3 = lcg_step(a2), b3 = lcg_step(b2);
+    sa = ((u64)a3.hi << 32) | (u64)a3.lo;
+    sb = ((u64)b3.hi << 32) | (u64)b3.lo;
     return attempt2_draws<KR0>(a1, a2, a3, b1, b2, b3, n, kR);
 }
 template <bool KR0>
@@ -2516,9 +2531,48 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 u64 jA, jG;
                 jread(J.j24, lane, jA, jG);
                 const u64 s_lane = jA * rng.st + jG;
-                u64 sk = s_lane;
                 int tf = 0;
                 u64 Aor = 0ull, K[PT_KATT];
+#if PT_LM_CHAINS == 2
+                /* two independent chains per lane: attempts k and k + KATT/2
+                 * as one packed pair, the second chain starting 3 KATT/2
+                 * draws into the lane's stream (one jump), so the pair's
+                 * engine steps do not wait on each other; tfa / tfb = the
+                 * trailing failures of each half, ab = the lane accepted in
+                 * the second half */
+                constexpr int HK = PT_KATT / 2;
+                u64 sa = s_lane, sb;
+                {
+                    u64 hA, hG;
+                    jread(J.j3, HK, hA, hG);
+                    sb = hA * s_lane + hG;
+                }
+                int tfb = 0, ab = 0;
+#pragma unroll
+                for (int k = 0; k < HK; k++) {
+                    const Attempt2 ap = attempt2_split<KR0>(sa, sb, n, kR);
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int kk = k + h * HK;
+                        const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
+                        u64 D = 0ull;
+                        if (RAW)
+                            D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
+                        K[kk] = ap.A[h] & ~D;
+                        ta += __popcll(ap.A[h]);
+                        tk += __popcll(K[kk]);
+                        Aor |= ap.A[h];
+                        if (h) {
+                            tfb = zero_if(ap.A[h], add_lane_bit(tfb, ap.F[h]));
+                            ab = mask_sel(ap.A[h], 1, ab);
+                        } else {
+                            tf = zero_if(ap.A[h], add_lane_bit(tf, ap.F[h]));
+                        }
+                    }
+                }
+                tf = ab ? tfb : tf + tfb;
+#else
+                u64 sk = s_lane;
 #pragma unroll
                 for (int k = 0; k < PT_KATT; k += 2) {
                     const Attempt2 ap = attempt2_chain<KR0>(sk, n, kR);
@@ -2535,6 +2589,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         tf = zero_if(ap.A[h], add_lane_bit(tf, ap.F[h]));
                     }
                 }
+#endif
                 /* ring entries, numbered in child order */
                 int slot = nkeep;
 #pragma unroll
