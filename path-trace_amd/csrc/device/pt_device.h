@@ -1311,6 +1311,10 @@ template <class R>
 __device__ __forceinline__ bool first_hit(const typename R::Ctx &ctx, V3 d, const Env &e, float &t, u32 &ref,
                                           bool &exit_hit)
 {
+#ifdef PT_MERGE_STUB /* diagnostic builds only: every lazy merge left out (wrong bits) */
+    (void)ctx, (void)d, (void)e, (void)t, (void)ref, (void)exit_hit;
+    return false;
+#endif
     typename R::St st;
     R::init(st, ctx, mkray(d), e);
     CS s;
@@ -2845,8 +2849,12 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     u32 ref;
                     bool ex;
                     V3 col = mk(0, 0, 0);
+#ifndef PT_SLOW_STUB /* diagnostic builds only: the slow pass's merge left out (wrong bits) */
                     if (first_hit<typename S::Root>(ctx, dir, e, t, ref, ex))
                         col = S::emis(ref_mat(ref), hit + t * dir, e);
+#else
+                    (void)ctx, (void)t, (void)ref, (void)ex;
+#endif
                     const V3 term = ((aN * en.w) * rc) * col;
                     ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
                 }
