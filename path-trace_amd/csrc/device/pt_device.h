@@ -82,6 +82,8 @@ struct PtLaunch
                            (origin, direction, strength) -- traceRay's arguments,
                            include/path-trace.h:59 -- instead of a camera ray    */
     long long ray0;     /* PT_RAYS: engine key index of slot 0 (slot k: ray0 + k) */
+    int grab;           /* chunks a wave takes per work-queue atomic while plenty are
+                           left (1 near the end of the launch); >= 1               */
 };
 /* The engine key index of a slot's item: its pixel index, or in a ray-list
  * module the caller's ray index */
@@ -3907,25 +3909,42 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
-    auto dequeue = [&]() {
+    /* The queue is one device-scope counter of chunks.  A single address takes
+     * on the order of 10^8 atomics per second across the 8 XCDs, which caps
+     * scenes of cheap samples (C5: 64-sample chunks at ~85 M/s); so a wave
+     * takes a run of lp.grab chunks per atomic while more than 8 runs per wave
+     * remain, then single chunks, which keeps the launch's tail short.  The
+     * order of the items does not change any result. */
+    const long long nwaves = (long long)gridDim.x * PT_WPW;
+    const int GRAB = lp.grab > 1 ? lp.grab : 1;
+    auto want = [&](long long from) { /* run length of the next request, seen from chunk `from` */
+        return (GRAB > 1 && n_chunks - from > 8ll * GRAB * nwaves) ? GRAB : 1;
+    };
+    auto dequeue = [&](int k) {
         long long c = 0;
         if (lane == 0)
-            c = (long long)atomicAdd(work, 1ull);
+            c = (long long)atomicAdd(work, (u64)k);
         return c;
     };
     auto uniform_chunk = [&](long long c) {
         return ((long long)uni((int)(c >> 32)) << 32) | (long long)(u32)uni((int)c);
     };
-    long long next = dequeue();
+    int nk = want(0), left = 0;  /* nk: length of the run `next` starts; left: chunks left in this run */
+    long long next = dequeue(nk), run = 0;
     for (;;) {
-        const long long chunk = uniform_chunk(next);
+        if (left == 0) {
+            run = uniform_chunk(next);
+            left = nk;
+#if PT_DEQUEUE_PREFETCH
+            /* the next run's dequeue is in flight while this one is traced */
+            nk = want(run + left);
+            next = dequeue(nk);
+#endif
+        }
+        const long long chunk = run++;
+        left--;
         if (chunk >= n_chunks)
             break;
-#if PT_DEQUEUE_PREFETCH
-        /* the next chunk's dequeue is in flight while this one is traced (one
-         * contended device atomic per chunk, ~1-3 us with every wave pulling) */
-        next = dequeue();
-#endif
         const long long item0 = chunk * CH;
         PT_T0(tchunk);
         /* the chunk's camera queries, one per lane */
@@ -4009,7 +4028,10 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         const V3 mine = mk(__uint_as_float(mr.x), __uint_as_float(mr.y), __uint_as_float(mr.z));
         PT_T0(tout);
 #if !PT_DEQUEUE_PREFETCH
-        next = dequeue();
+        if (left == 0) {
+            nk = want(run);
+            next = dequeue(nk);
+        }
 #endif
         const long long my = item0 + lane;
         if (lp.block_sums) {

@@ -75,6 +75,7 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     long long perm;
     const float *rays;
     long long ray0;
+    int grab;
 };
 
 template <class T>
@@ -589,6 +590,20 @@ long long slot_permutation(long long nslots)
     return 0;
 }
 
+/* Chunks a wave takes per work-queue atomic while plenty are left (pt_device.h
+ * render_chunk); PT_GRAB=n is an experiment hook. */
+int grab_chunks()
+{
+    static const int g = [] {
+        const char *env = getenv("PT_GRAB");
+        if (!env || !*env)
+            return 8;
+        fprintf(stderr, "pt: experiment hook PT_GRAB=%s active\n", env);
+        return std::max(1, std::min(64, atoi(env)));
+    }();
+    return g;
+}
+
 /* Stage floats for the largest launch of a render: block partials for
  * slot-major whole-block launches, else one value per sample -- launches of
  * <= 64 samples per slot (sample-major) and small launches whose chunks fall
@@ -799,6 +814,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
                 (block_staging(p) && !lp.sample_major && (chunk == 32 || chunk == 64) && nsamp % chunk == 0) ? 1 : 0;
             lp.rays = rays;
             lp.ray0 = ray0;
+            lp.grab = grab_chunks();
             reduce_mode = p->order == PT_ORDER_REFERENCE ? 0 : lp.block_sums ? 2 : 1;
             ds.stage.ensure((size_t)(lp.block_sums ? npix * (nsamp / 32) * 3 : npix * nsamp * 3));
             const float *Pp = ds.P.p;
