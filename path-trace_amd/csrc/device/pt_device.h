@@ -1420,29 +1420,6 @@ __device__ __forceinline__ bool lane_first_hit(const typename R::Ctx &ctx, V3 d,
 #endif
 }
 
-/* A lane's own query without the lazy merge: the spans and the fast checks
- * only.  Returns whether they decide the query (hit, t, ref, exit_hit valid);
- * where they do not, a lane walk gives its sample back to the wave
- * (PT_LANE_HANDBACK), whose spine runs the merge -- so the merge's iterator
- * state is not live beside the lane walk's registers. */
-template <class R>
-__device__ __forceinline__ int lane_fast_hit(const typename R::Ctx &ctx, V3 d, const Env &e, bool &hit, float &t,
-                                             u32 &ref, bool &exit_hit)
-{
-    PrimSpans<R::HI> ps;
-    R::span(ps, ctx, mkray(d), e);
-    return span_first_hit<R>(ps, hit, t, ref, exit_hit);
-}
-/* The lane paths hand undecided queries back to the wave: on by default
- * where lanes walk whole trees (their registers are the kernel's peak) */
-#ifndef PT_LANE_HANDBACK
-#if defined(PT_LANE_WALK) || defined(PT_LANE_SCATTER)
-#define PT_LANE_HANDBACK 1
-#else
-#define PT_LANE_HANDBACK 0
-#endif
-#endif
-
 /* Fast first hit over precomputed primitive spans; valid when R::fast_ok. */
 template <class R, class PS>
 __device__ __forceinline__ bool fast_first_hit(const PS &ps, float &t, int &mat)
@@ -2084,27 +2061,6 @@ __device__ __forceinline__ T lds_get_v(const LdsBox<T> &b)
     }
     return u.t;
 }
-/* the same, each word made a scalar (readfirstlane): for a struct that is
- * uniform by construction (the burst origin's primitive contexts), so that
- * code whose vector registers are scarce -- the slow pass's lazy merge --
- * reads it from SGPRs instead of holding a vector copy */
-template <class T>
-__device__ __forceinline__ T lds_get_s(const LdsBox<T> &b)
-{
-    union
-    {
-        float4 w[LdsBox<T>::N];
-        u32 u[4 * LdsBox<T>::N];
-        T t;
-    } x;
-#pragma unroll
-    for (int i = 0; i < LdsBox<T>::N; i++)
-        x.w[i] = b.w[i];
-#pragma unroll
-    for (int i = 0; i < (int)((sizeof(T) + 3) / 4); i++)
-        x.u[i] = (u32)__builtin_amdgcn_readfirstlane((int)x.u[i]);
-    return x.t;
-}
 template <class T>
 __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 {
@@ -2157,9 +2113,6 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 #define PT_LM_CHAINS 1 /* lane-major rounds: engine chains per lane (2: the halves interleaved) */
 #endif
 
-#ifndef PT_SLOW_CTX_SGPR
-#define PT_SLOW_CTX_SGPR 1 /* the slow pass reads the burst origin's contexts into SGPRs (lds_get_s) */
-#endif
 #ifndef PT_PASS_PAIR_FALLBACK
 /* 0: in a burst's fast pass over a Difference-free tree, lanes the one-pass
  * check cannot decide go to the full merge directly instead of through the
@@ -2893,11 +2846,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                     const int pos = slot_pos(slowq[(s_head + lane) & (PT_SCAP - 1)]);
                     const float4 en = ring[pos & (PT_RCAP - 1)];
                     const V3 dir = mk(en.x, en.y, en.z);
-#if PT_SLOW_CTX_SGPR
-                    const typename S::Root::Ctx ctx = lds_get_s(*cxp);
-#else
                     const typename S::Root::Ctx ctx = lds_get(*cxp);
-#endif
                     float t;
                     u32 ref;
                     bool ex;
@@ -3140,7 +3089,6 @@ struct CamHit
     float t;
     u32 ref;
     int ex;
-    int valid; /* 0: the lane's checks could not decide it (PT_LANE_HANDBACK): the spine queries it */
 };
 
 /* tracePixel's jittered camera ray (path-trace.h:190-198): two draws */
@@ -3210,16 +3158,8 @@ __device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 o, V3 d,
     u32 ref2 = 0;
     bool ex2 = false;
     V3 col = mk(0, 0, 0);
-#if PT_LANE_HANDBACK
-    bool h2 = false;
-    if (!lane_fast_hit<typename S::Root>(ctx, refl, e, h2, t2, ref2, ex2))
-        return false;
-    if (h2)
-        col = S::emis(ref_mat(ref2), hit + t2 * refl, e);
-#else
     if (lane_first_hit<typename S::Root>(ctx, refl, e, t2, ref2, ex2))
         col = S::emis(ref_mat(ref2), hit + t2 * refl, e);
-#endif
     res = (z + (retval + w * col)) / 1.0f;
     return true;
 }
@@ -3285,16 +3225,7 @@ __device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 o0, V3 d0
             } else {
                 typename S::Root::Ctx ctx;
                 S::Root::prep_l(ctx, o, e);
-#if PT_LANE_HANDBACK
-                bool h = false;
-                if (!lane_fast_hit<typename S::Root>(ctx, d, e, h, t, ref, ex)) {
-                    ok = false; /* the wave walks this sample */
-                    continue;
-                }
-                found = h;
-#else
                 found = lane_first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
-#endif
             }
             if (!found) {
                 r = mk(0, 0, 0);
@@ -3499,14 +3430,7 @@ __device__ __forceinline__ bool lane_walk_sc(const Env &e, int depth0, V3 o0, V3
             } else {
                 typename S::Root::Ctx ctx;
                 S::Root::prep_l(ctx, o, e);
-#if PT_LANE_HANDBACK
-                bool h = false;
-                if (!lane_fast_hit<typename S::Root>(ctx, d, e, h, t, ref, ex))
-                    return false; /* the wave walks this sample */
-                found = h;
-#else
                 found = lane_first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
-#endif
             }
             if (!found) {
                 r = mk(0, 0, 0);
@@ -3631,16 +3555,8 @@ __device__ __forceinline__ bool lane_walk_sc(const Env &e, int depth0, V3 o0, V3
                 u32 ref = 0;
                 bool ex = false;
                 V3 col = mk(0, 0, 0);
-#if PT_LANE_HANDBACK
-                bool h = false;
-                if (!lane_fast_hit<typename S::Root>(ctx, nd, e, h, t, ref, ex))
-                    return false; /* the wave walks this sample */
-                if (h)
-                    col = S::emis(ref_mat(ref), c.hit + t * nd, e);
-#else
                 if (lane_first_hit<typename S::Root>(ctx, nd, e, t, ref, ex))
                     col = S::emis(ref_mat(ref), c.hit + t * nd, e);
-#endif
                 const V3 term = ((aN * factor) * c.rc) * col;
                 if (STRICT)
                     c.part = c.part + term;
@@ -3713,7 +3629,7 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
             u32 ref = 0;
             bool ex = false;
             bool found;
-            if (sp == 0 && cam.valid) {
+            if (sp == 0) {
                 found = cam.hit != 0, t = cam.t, ref = cam.ref, ex = cam.ex != 0;
             } else {
                 PT_T0(tq);
@@ -4032,7 +3948,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         const long long item0 = chunk * CH;
         PT_T0(tchunk);
         /* the chunk's camera queries, one per lane */
-        CamHit ch = {0, 0.0f, 0u, 0, 1};
+        CamHit ch = {0, 0.0f, 0u, 0};
         int ldone = 0, lq = 0, lsh = 0;
         int lpix = 0, ls = 0; /* the lane's (pixel, sample), read by the wave loop below */
         V3 lres = mk(0, 0, 0);
@@ -4059,24 +3975,15 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             S::Root::prep(ctx, o, e);
 #endif
             bool ex = false;
-#if PT_LANE_HANDBACK
-            bool h = false;
-            ch.valid = lane_fast_hit<typename S::Root>(ctx, d, e, h, ch.t, ch.ref, ex) ? 1 : 0;
-            ch.hit = h ? 1 : 0;
-#else
             ch.hit = lane_first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
-            ch.valid = 1;
-#endif
             ch.ex = ex ? 1 : 0;
-            if (ch.valid) {
 #if defined(PT_LANE_SCATTER) /* per scene, pt_scene_set_lane_scatter */
-                ldone = lane_walk_sc<S, MAXD, STRICT>(e, lp.depth, o, d, str, ch, r, lres, lq, lsh) ? 1 : 0;
+            ldone = lane_walk_sc<S, MAXD, STRICT>(e, lp.depth, o, d, str, ch, r, lres, lq, lsh) ? 1 : 0;
 #elif defined(PT_LANE_WALK) /* per scene, pt_scene_set_lane_walk */
-                ldone = lane_walk<S>(e, lp.depth, o, d, str, ch, lres, lq, lsh) ? 1 : 0;
+            ldone = lane_walk<S>(e, lp.depth, o, d, str, ch, lres, lq, lsh) ? 1 : 0;
 #else
-                ldone = lane_sample<S>(e, lp.depth, o, d, str, ch, lres, lq, lsh) ? 1 : 0;
+            ldone = lane_sample<S>(e, lp.depth, o, d, str, ch, lres, lq, lsh) ? 1 : 0;
 #endif
-            }
         }
         PT_ACC2(cnt, 1, tchunk); /* the lane-parallel front end */
         {
@@ -4100,9 +4007,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         /* park the lanes' state in LDS for the walks below */
         uint4 *const lb = lbuf[wave];
         const bool lwalk = lvalid && !ldone;
-        /* sample index < 2^20 (engine key layout): bit 29 = camera query undecided */
-        lb[lane] = lwalk ? make_uint4((u32)lpix,
-                                      (u32)ls | ((u32)ch.hit << 30) | ((u32)ch.ex << 31) | ((u32)!ch.valid << 29),
+        lb[lane] = lwalk ? make_uint4((u32)lpix, (u32)ls | ((u32)ch.hit << 30) | ((u32)ch.ex << 31),
                                       __float_as_uint(ch.t), ch.ref)
                          : make_uint4(__float_as_uint(lres.x), __float_as_uint(lres.y), __float_as_uint(lres.z), 0u);
         /* the other items, one after another by the whole wave; only this mask
@@ -4112,9 +4017,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             PT_T0(tt);
             const uint4 q = lb[j];
             const int qy = uni((int)q.y);
-            const CamHit cam = {(qy >> 30) & 1, unif(__uint_as_float(q.z)), (u32)uni((int)q.w), (int)((u32)qy >> 31),
-                                !((qy >> 29) & 1)};
-            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni((int)q.x), qy & 0x1FFFFFFF, stk[wave], L, jump, jl, cnt,
+            const CamHit cam = {(qy >> 30) & 1, unif(__uint_as_float(q.z)), (u32)uni((int)q.w), (int)((u32)qy >> 31)};
+            V3 c = trace_sample<S, MAXD, STRICT>(e, lp, uni((int)q.x), qy & 0x3FFFFFFF, stk[wave], L, jump, jl, cnt,
                                                  cam);
             PT_ACC(cnt, 6, tt);
             if (lane == j)
