@@ -229,6 +229,16 @@ __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
     }
     return q;
 }
+/* normalize() where the device library needs it (normals, reflect / refract,
+ * the sky maps): the exact fast sequence (same bits) unless PT_FAST_NORM=0 */
+#ifndef PT_FAST_NORM
+#define PT_FAST_NORM 1
+#endif
+#if PT_FAST_NORM
+#define PT_NORM(v) cnormalize(v)
+#else
+#define PT_NORM(v) normalize(v)
+#endif
 /* (int)x as x86 cvttss2si: out-of-range and NaN give INT_MIN (the reference
  * runs on x86; v_cvt_i32_f32 would saturate / give 0). */
 __device__ __forceinline__ int cvt_x86(float x)
@@ -243,7 +253,7 @@ __device__ __forceinline__ float clamp01(float x)
 /* Vector3D::reflect, vector3d.h:186-190 */
 __device__ __forceinline__ V3 reflect(V3 d, V3 n)
 {
-    n = normalize(n);
+    n = PT_NORM(n);
     return d - (2.0f * dot(d, n)) * n;
 }
 __device__ __forceinline__ bool bad_ior(float ior, V3 n, V3 d)
@@ -256,8 +266,8 @@ __device__ __forceinline__ float refract_strength(V3 d, float ior, V3 n)
 {
     if (bad_ior(ior, n, d))
         return 0.0f;
-    n = normalize(n);
-    V3 inc = normalize(d);
+    n = PT_NORM(n);
+    V3 inc = PT_NORM(d);
     float c = dot(inc, n);
     float r = 1.0f - ior * ior * (1.0f - c * c);
     if (r <= 0.0f)
@@ -269,13 +279,17 @@ __device__ __forceinline__ V3 refract(V3 d, float ior, V3 n)
 {
     if (bad_ior(ior, n, d))
         return mk(0, 0, 0);
-    n = normalize(n);
-    V3 inc = normalize(d);
+    n = PT_NORM(n);
+    V3 inc = PT_NORM(d);
     float c = dot(inc, n);
     float arg = 1.0f - ior * ior * (1.0f - c * c);
     if (arg < 0.0f)
         return mk(0, 0, 0);
-    return normalize(ior * inc - (ior * c + __builtin_sqrtf(arg)) * n);
+#if PT_FAST_NORM
+    return PT_NORM(ior * inc - (ior * c + csqrt(arg)) * n);
+#else
+    return PT_NORM(ior * inc - (ior * c + __builtin_sqrtf(arg)) * n);
+#endif
 }
 /* Matrix::apply / applyNoTranslate, transform.h:408-421; m in ctor order */
 __device__ __forceinline__ V3 m_apply(const float *__restrict__ m, V3 v)
@@ -718,7 +732,7 @@ struct Sph
     __device__ static __forceinline__ int fast_ok(const PS &) { return 1; }
     __device__ static __forceinline__ V3 normal(int, float t, V3 o, V3 d, const Env &e)
     {
-        return normalize((o + t * d) - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+        return PT_NORM((o + t * d) - mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
     /* Sound test on an UNNORMALISED direction w that the span of normalize(w)
      * is dead or ends before EPS (the generation round's dark test).  Origin
@@ -849,7 +863,7 @@ struct Pln
     __device__ static __forceinline__ int fast_ok(const PS &) { return 1; }
     __device__ static __forceinline__ V3 normal(int, float, V3, V3, const Env &e)
     {
-        return normalize(mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+        return PT_NORM(mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
     }
     /* Sound dark test on an unnormalised direction w (see Sph::dark_mask).
      * With num <= -1e-6 the span of normalize(w) is dead or ends before EPS
@@ -1295,7 +1309,7 @@ struct Xf
     __device__ static __forceinline__ V3 normal(int prim, float t, V3 o, V3 d, const Env &e)
     {
         V3 n = C::normal(prim, t, m_apply(e.P + MOFF, o), m_lin(e.P + MOFF, d), e);
-        return normalize(m_lin(e.P + IOFF, n));
+        return PT_NORM(m_lin(e.P + IOFF, n));
     }
     /* no raw-direction dark test through a transform unless nothing inside is selected */
     template <class SEL>
@@ -1805,13 +1819,22 @@ __device__ __forceinline__ V3 mirrorball_map(V3 v) /* transform_texture.h:46-59 
 {
     if (is_zero(v))
         return mk(0, 0, 0);
-    v = normalize(v);
+    v = PT_NORM(v);
     if (v.z <= -1.0f)
         return mk(0, 0.5f, 0);
+#if PT_FAST_NORM /* csqrt / cdiv: the same bits as sqrtf and '/' */
+    float d = csqrt(2.0f + 2.0f * v.z);
+    if (d == 0.0f)
+        return mk(0, 0.5f, 0);
+    const Rcp rd = mkrcp(d);
+    const bool dok = den_ok(d);
+    float xt = cdiv(v.x, rd, dok), yt = cdiv(v.y, rd, dok);
+#else
     float d = __builtin_sqrtf(2.0f + 2.0f * v.z);
     if (d == 0.0f)
         return mk(0, 0.5f, 0);
     float xt = v.x / d, yt = v.y / d;
+#endif
     return mk((float)((double)xt * 0.5 + 0.5), (float)((double)yt * 0.5 + 0.5), 0);
 }
 /* The reference's std::atan2(float, float) and std::asin(float) are glibc's
@@ -1939,7 +1962,7 @@ __device__ __forceinline__ V3 spherical_map(V3 v) /* transform_texture.h:73-85 *
     const double PI = 3.14159265358979323846;
     if (is_zero(v))
         return mk(0, 0, 0);
-    v = normalize(v);
+    v = PT_NORM(v);
     float theta = libm_atan2f(v.y, v.x);
     if ((double)theta < -PI)
         theta = (float)((double)theta + 2 * PI);
