@@ -13,6 +13,8 @@
 #   defs:SPP:REPS:D1|D2   the same for PT_DEVICE_DEFINES variants (tools/ab/defs.sh)
 #   cfg:CFG,NPIX,SPP:REPS:S1|S2   A/B on tools/cfg_probe.py (hashed pixels of a config); a spec
 #                         is "-" or VAR=value[,VAR=value] (PT_DEVICE_HEADER=..., PT_DEVICE_DEFINES=...)
+#   benchab:CFG:REPS:S1|S2   whole bench.py runs (--no-cpu) under env specs, interleaved
+#                         (tools/ab/bench_env.sh; spec "-" or VAR=value[,VAR=value])
 #   phase:SPP             PT_PHASE_TIMING phase split of the C3 frame (tools/phase_probe.py)
 #   evidence:CFG          the bench line's evidence, bound to the timed code object:
 #                         PMC passes (tools/pmc_bench.sh) -> profiles/round5/pmc_bench_CFG.json,
@@ -60,6 +62,9 @@ for step in "$@"; do
     IFS='|' read -r -a SP <<< "$c"
     run 1200 "$OUT/cfg_${a//,/_}.txt" bash tools/ab/cfg_hdr_ab.sh "$OUT/cfgp" "$b" "${a//,/ }" "${SP[@]}"
     cat "$OUT/cfg_${a//,/_}.txt" ;;
+  benchab)
+    IFS='|' read -r -a SP <<< "$c"
+    run 1500 "$OUT/benchab_$a.txt" bash tools/ab/bench_env.sh "$a" "$b" "${SP[@]}"; cat "$OUT/benchab_$a.txt" ;;
   phase)
     run 600 "$OUT/phase_$a.txt" python3 tools/phase_probe.py "$a"; cat "$OUT/phase_$a.txt" ;;
   evidence)
