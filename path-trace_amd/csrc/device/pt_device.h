@@ -230,9 +230,15 @@ __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
     return q;
 }
 /* normalize() where the device library needs it (normals, reflect / refract,
- * the sky maps): the exact fast sequence (same bits) unless PT_FAST_NORM=0 */
+ * the spherical sky map): PT_FAST_NORM=1 takes the exact fast sequence (same
+ * bits).  Off: same-box A/B (profiles/round5/ab_grab_fastnorm_c3_full.txt)
+ * C5 -3.6 % (its lane walks carry the extra branches), C3 -0.8 %, C2 +1.2 %
+ * -- the mirror-ball map's part, which PT_FAST_MIRRORBALL keeps */
 #ifndef PT_FAST_NORM
-#define PT_FAST_NORM 1
+#define PT_FAST_NORM 0
+#endif
+#ifndef PT_FAST_MIRRORBALL
+#define PT_FAST_MIRRORBALL 1
 #endif
 #if PT_FAST_NORM
 #define PT_NORM(v) cnormalize(v)
@@ -1819,10 +1825,14 @@ __device__ __forceinline__ V3 mirrorball_map(V3 v) /* transform_texture.h:46-59 
 {
     if (is_zero(v))
         return mk(0, 0, 0);
+#if PT_FAST_MIRRORBALL /* cnormalize / csqrt / cdiv: the same bits as normalize, sqrtf and '/' */
+    v = cnormalize(v);
+#else
     v = PT_NORM(v);
+#endif
     if (v.z <= -1.0f)
         return mk(0, 0.5f, 0);
-#if PT_FAST_NORM /* csqrt / cdiv: the same bits as sqrtf and '/' */
+#if PT_FAST_MIRRORBALL
     float d = csqrt(2.0f + 2.0f * v.z);
     if (d == 0.0f)
         return mk(0, 0.5f, 0);
@@ -3825,6 +3835,9 @@ __device__ __forceinline__ void item_slot(const PtLaunch &lp, long long item, lo
  * joins the chunk's first load).  Same-box A/B, round 4
  * (profiles/round4/ab_knobs_r4u.txt): C3 -0.5 %, C5 (lane walks) +0.36 %:
  * on for lane-walk scenes */
+#ifndef PT_GRAB_TICKS
+#define PT_GRAB_TICKS 20000 /* 200 us per chunk at the 100 MHz real-time clock */
+#endif
 #ifndef PT_DEQUEUE_PREFETCH
 #if defined(PT_LANE_WALK)
 #define PT_DEQUEUE_PREFETCH 1
@@ -3934,14 +3947,17 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
     /* The queue is one device-scope counter of chunks.  A single address takes
      * on the order of 10^8 atomics per second across the 8 XCDs, which caps
-     * scenes of cheap samples (C5: 64-sample chunks at ~85 M/s); so a wave
-     * takes a run of lp.grab chunks per atomic while more than 8 runs per wave
-     * remain, then single chunks, which keeps the launch's tail short.  The
-     * order of the items does not change any result. */
+     * scenes of cheap samples (C5: 64-sample chunks at ~85 M/s).  So a wave
+     * whose last run of chunks took under PT_GRAB_TICKS (100 MHz ticks) per
+     * chunk takes a run of lp.grab chunks per atomic, while more than 8 runs
+     * per wave remain; otherwise single chunks (C3's expensive chunks lose
+     * 6.6 % with runs of 8 -- profiles/round5/ab_grab_fastnorm_c3_full.txt --
+     * and gain nothing from them).  The order of the items changes no result. */
     const long long nwaves = (long long)gridDim.x * PT_WPW;
     const int GRAB = lp.grab > 1 ? lp.grab : 1;
+    int cheap = 0; /* the last run took under PT_GRAB_TICKS per chunk (unknown: single chunks) */
     auto want = [&](long long from) { /* run length of the next request, seen from chunk `from` */
-        return (GRAB > 1 && n_chunks - from > 8ll * GRAB * nwaves) ? GRAB : 1;
+        return (GRAB > 1 && cheap && n_chunks - from > 8ll * GRAB * nwaves) ? GRAB : 1;
     };
     auto dequeue = [&](int k) {
         long long c = 0;
@@ -3952,12 +3968,14 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     auto uniform_chunk = [&](long long c) {
         return ((long long)uni((int)(c >> 32)) << 32) | (long long)(u32)uni((int)c);
     };
-    int nk = want(0), left = 0;  /* nk: length of the run `next` starts; left: chunks left in this run */
+    int nk = 1, left = 0, cur = 1; /* nk: length of the run `next` starts; left: chunks left in this run */
     long long next = dequeue(nk), run = 0;
+    u64 t_run = 0;
     for (;;) {
         if (left == 0) {
             run = uniform_chunk(next);
-            left = nk;
+            left = cur = nk;
+            t_run = __builtin_amdgcn_s_memrealtime();
 #if PT_DEQUEUE_PREFETCH
             /* the next run's dequeue is in flight while this one is traced */
             nk = want(run + left);
@@ -4050,12 +4068,13 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         const uint4 mr = lb[lane];
         const V3 mine = mk(__uint_as_float(mr.x), __uint_as_float(mr.y), __uint_as_float(mr.z));
         PT_T0(tout);
-#if !PT_DEQUEUE_PREFETCH
         if (left == 0) {
+            cheap = __builtin_amdgcn_s_memrealtime() - t_run < (u64)PT_GRAB_TICKS * (u64)cur;
+#if !PT_DEQUEUE_PREFETCH
             nk = want(run);
             next = dequeue(nk);
-        }
 #endif
+        }
         const long long my = item0 + lane;
         if (lp.block_sums) {
             /* the chunk is one 32-sample block of one slot (slot-major, chunk
