@@ -237,8 +237,8 @@ __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
 #ifndef PT_FAST_NORM
 #define PT_FAST_NORM 0
 #endif
-#ifndef PT_FAST_MIRRORBALL
-#define PT_FAST_MIRRORBALL 1
+#ifndef PT_FAST_MIRRORBALL /* off: same-box C2 A/B -2.4 % .. +1.2 % (noise), profiles/round5/ab_grab_adaptive.txt */
+#define PT_FAST_MIRRORBALL 0
 #endif
 #if PT_FAST_NORM
 #define PT_NORM(v) cnormalize(v)
@@ -3950,9 +3950,11 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
      * scenes of cheap samples (C5: 64-sample chunks at ~85 M/s).  So a wave
      * whose last run of chunks took under PT_GRAB_TICKS (100 MHz ticks) per
      * chunk takes a run of lp.grab chunks per atomic, while more than 8 runs
-     * per wave remain; otherwise single chunks (C3's expensive chunks lose
-     * 6.6 % with runs of 8 -- profiles/round5/ab_grab_fastnorm_c3_full.txt --
-     * and gain nothing from them).  The order of the items changes no result. */
+     * per wave remain; otherwise single chunks.  The runtime asks for runs only
+     * in lane-walk scenes, whose chunks are uniformly cheap (C5 +53 %); C3's mix
+     * of cheap and expensive chunks loses with them (runs of 8 throughout:
+     * -6.6 %, adaptive: -0.45 %, profiles/round5/ab_grab_*.txt) and is far from
+     * the atomic's rate.  The order of the items changes no result. */
     const long long nwaves = (long long)gridDim.x * PT_WPW;
     const int GRAB = lp.grab > 1 ? lp.grab : 1;
     int cheap = 0; /* the last run took under PT_GRAB_TICKS per chunk (unknown: single chunks) */

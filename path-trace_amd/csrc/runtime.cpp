@@ -590,18 +590,23 @@ long long slot_permutation(long long nslots)
     return 0;
 }
 
-/* Chunks a wave takes per work-queue atomic while plenty are left (pt_device.h
- * render_chunk); PT_GRAB=n is an experiment hook. */
-int grab_chunks()
+/* Chunks a wave takes per work-queue atomic while its chunks are cheap and
+ * plenty are left (pt_device.h render_chunk): 8 in lane-walk scenes, whose
+ * chunks are uniformly cheap and whose launches the single counter's atomic
+ * rate bounds (C5 5 296 -> 8 112 Msamples/s), 1 elsewhere (C3: -0.45 % with
+ * runs).  PT_GRAB=n is an experiment hook. */
+int grab_chunks(const SceneImpl &s)
 {
-    static const int g = [] {
+    static const int env_g = [] {
         const char *env = getenv("PT_GRAB");
         if (!env || !*env)
-            return 8;
+            return 0;
         fprintf(stderr, "pt: experiment hook PT_GRAB=%s active\n", env);
         return std::max(1, std::min(64, atoi(env)));
     }();
-    return g;
+    if (env_g)
+        return env_g;
+    return (s.lane_walk > 0 || s.lane_scatter) ? 8 : 1;
 }
 
 /* Stage floats for the largest launch of a render: block partials for
@@ -814,7 +819,7 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
                 (block_staging(p) && !lp.sample_major && (chunk == 32 || chunk == 64) && nsamp % chunk == 0) ? 1 : 0;
             lp.rays = rays;
             lp.ray0 = ray0;
-            lp.grab = grab_chunks();
+            lp.grab = grab_chunks(s);
             reduce_mode = p->order == PT_ORDER_REFERENCE ? 0 : lp.block_sums ? 2 : 1;
             ds.stage.ensure((size_t)(lp.block_sums ? npix * (nsamp / 32) * 3 : npix * nsamp * 3));
             const float *Pp = ds.P.p;
