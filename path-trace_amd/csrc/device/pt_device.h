@@ -3835,6 +3835,15 @@ __device__ __forceinline__ void item_slot(const PtLaunch &lp, long long item, lo
  * joins the chunk's first load).  Same-box A/B, round 4
  * (profiles/round4/ab_knobs_r4u.txt): C3 -0.5 %, C5 (lane walks) +0.36 %:
  * on for lane-walk scenes */
+/* the run-taking work queue, compiled where the runtime asks for runs
+ * (lane-walk scenes); other scenes keep one chunk per atomic */
+#ifndef PT_GRAB_RUNS
+#if defined(PT_LANE_WALK) || defined(PT_LANE_SCATTER)
+#define PT_GRAB_RUNS 1
+#else
+#define PT_GRAB_RUNS 0
+#endif
+#endif
 #ifndef PT_GRAB_TICKS
 #define PT_GRAB_TICKS 20000 /* 200 us per chunk at the 100 MHz real-time clock */
 #endif
@@ -3950,11 +3959,15 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
      * scenes of cheap samples (C5: 64-sample chunks at ~85 M/s).  So a wave
      * whose last run of chunks took under PT_GRAB_TICKS (100 MHz ticks) per
      * chunk takes a run of lp.grab chunks per atomic, while more than 8 runs
-     * per wave remain; otherwise single chunks.  The runtime asks for runs only
-     * in lane-walk scenes, whose chunks are uniformly cheap (C5 +53 %); C3's mix
+     * per wave remain; otherwise single chunks.  Built (PT_GRAB_RUNS) and asked
+     * for only in lane-walk scenes, whose chunks are uniformly cheap (C5 +53 %); C3's mix
      * of cheap and expensive chunks loses with them (runs of 8 throughout:
      * -6.6 %, adaptive: -0.45 %, profiles/round5/ab_grab_*.txt) and is far from
      * the atomic's rate.  The order of the items changes no result. */
+    auto uniform_chunk = [&](long long c) {
+        return ((long long)uni((int)(c >> 32)) << 32) | (long long)(u32)uni((int)c);
+    };
+#if PT_GRAB_RUNS
     const long long nwaves = (long long)gridDim.x * PT_WPW;
     const int GRAB = lp.grab > 1 ? lp.grab : 1;
     int cheap = 0; /* the last run took under PT_GRAB_TICKS per chunk (unknown: single chunks) */
@@ -3967,13 +3980,20 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             c = (long long)atomicAdd(work, (u64)k);
         return c;
     };
-    auto uniform_chunk = [&](long long c) {
-        return ((long long)uni((int)(c >> 32)) << 32) | (long long)(u32)uni((int)c);
-    };
     int nk = 1, left = 0, cur = 1; /* nk: length of the run `next` starts; left: chunks left in this run */
     long long next = dequeue(nk), run = 0;
     u64 t_run = 0;
+#else
+    auto dequeue = [&]() {
+        long long c = 0;
+        if (lane == 0)
+            c = (long long)atomicAdd(work, 1ull);
+        return c;
+    };
+    long long next = dequeue();
+#endif
     for (;;) {
+#if PT_GRAB_RUNS
         if (left == 0) {
             run = uniform_chunk(next);
             left = cur = nk;
@@ -3988,6 +4008,15 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         left--;
         if (chunk >= n_chunks)
             break;
+#else
+        const long long chunk = uniform_chunk(next);
+        if (chunk >= n_chunks)
+            break;
+#if PT_DEQUEUE_PREFETCH
+        /* the next chunk's dequeue is in flight while this one is traced */
+        next = dequeue();
+#endif
+#endif
         const long long item0 = chunk * CH;
         PT_T0(tchunk);
         /* the chunk's camera queries, one per lane */
@@ -4070,6 +4099,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         const uint4 mr = lb[lane];
         const V3 mine = mk(__uint_as_float(mr.x), __uint_as_float(mr.y), __uint_as_float(mr.z));
         PT_T0(tout);
+#if PT_GRAB_RUNS
         if (left == 0) {
             cheap = __builtin_amdgcn_s_memrealtime() - t_run < (u64)PT_GRAB_TICKS * (u64)cur;
 #if !PT_DEQUEUE_PREFETCH
@@ -4077,6 +4107,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             next = dequeue(nk);
 #endif
         }
+#elif !PT_DEQUEUE_PREFETCH
+        next = dequeue();
+#endif
         const long long my = item0 + lane;
         if (lp.block_sums) {
             /* the chunk is one 32-sample block of one slot (slot-major, chunk
