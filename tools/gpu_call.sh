@@ -44,8 +44,9 @@ for step in "$@"; do
     tail -1 "$OUT/smoke.log" ;;
   bench)
     IFS=, read -r -a EXTRA <<< "$b"
-    run 900 "$OUT/bench_$a.log" python3 bench.py --config "$a" "${EXTRA[@]}"
-    grep '^{' "$OUT/bench_$a.log" > "$OUT/bench_$a.json"; cut -c1-400 "$OUT/bench_$a.json" ;;
+    tag=$a; [ -n "$b" ] && tag="${a}_$(echo "$b" | tr -c 'A-Za-z0-9' '_')"
+    run 900 "$OUT/bench_$tag.log" python3 bench.py --config "$a" "${EXTRA[@]}"
+    grep '^{' "$OUT/bench_$tag.log" > "$OUT/bench_$tag.json"; cut -c1-400 "$OUT/bench_$tag.json" ;;
   dist)
     run 900 "$OUT/plain_$a.log" python3 bench.py --config "$a" --no-cpu --dump-frame "$OUT/plain_$a.npy"
     run 900 "$OUT/dist_$a.log" python3 bench.py --config "$a" --no-cpu --force-dist --dump-frame "$OUT/dist_$a.npy"
