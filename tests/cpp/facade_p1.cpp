@@ -165,6 +165,35 @@ int main(int argc, char **argv)
                                  ScreenHeight, (ScreenWidth < ScreenHeight ? ScreenWidth : ScreenHeight) * 2);
             if (!(c.x == c.x))
                 return 7;
+            /* the engine-less overload is the global FrameEngine's (run seed
+             * 0x5EED, fast order): Renderer::render's pixel */
+            Color g = tracePixel(*spanIterator, 3 % W, 1 % H, ScreenWidth, ScreenHeight, spp, depth, ScreenWidth,
+                                 ScreenHeight, (ScreenWidth < ScreenHeight ? ScreenWidth : ScreenHeight) * 2);
+            if (memcmp(&g, &img[(size_t)(1 % H) * W + 3 % W], sizeof(Color)))
+                return 15;
+            /* a reference-style engine T: two of its draws (high word first)
+             * are the call's run seed -- the same bits as a FrameEngine of that seed */
+            struct Lcg /* the reference's DefaultRandomEngine recurrence, include/path-trace.h:21-54 */
+            {
+                uint64_t v = 0x12476242;
+                static unsigned min() { return 0; }
+                static unsigned max() { return 0xFFFFFFFF; }
+                unsigned operator()() { return (unsigned)((v = 214013 * v + 2531011) >> 32); }
+            } lcg, twin;
+            Color t = tracePixel(*spanIterator, 2 % W, 2 % H, W, H, spp, depth, (float)W, (float)H,
+                                 (float)(2 * (W < H ? W : H)), lcg);
+            const uint64_t hi = twin(), lo = twin();
+            FrameEngine seeded((hi << 32) | lo);
+            Color u = tracePixel(*spanIterator, 2 % W, 2 % H, W, H, spp, depth, (float)W, (float)H,
+                                 (float)(2 * (W < H ? W : H)), seeded);
+            if (memcmp(&t, &u, sizeof(Color)) || lcg.v != twin.v)
+                return 16;
+            /* ... and successive calls draw fresh run seeds, as the reference's
+             * shared engine hands successive calls fresh numbers */
+            Color t2 = tracePixel(*spanIterator, 2 % W, 2 % H, W, H, spp, depth, (float)W, (float)H,
+                                  (float)(2 * (W < H ? W : H)), lcg);
+            if (lcg.v == twin.v || !(t2.x == t2.x))
+                return 17;
             /* a batch that holds the block corners x == W of every row: the
              * in-frame pixels keep their bits (keys never depend on the batch) */
             std::vector<int32_t> bx, by;

@@ -53,7 +53,12 @@ def test_facade_render_bitexact(facade_bin, tmp_path):
 def test_facade_trace_pixel_bitexact(facade_bin, tmp_path):
     """tracePixel(*spanIterator, x, y, W, H, spp, depth, sw, sh, dist, engine) per
     pixel -- the reference demo's call (src/test.cpp:450) against the facade --
-    gives Renderer::render's frame bit for bit (same run seed, fast order)."""
+    gives Renderer::render's frame bit for bit (same run seed, fast order).
+    The binary also checks the other two overloads (exit codes 15-17): the
+    engine-less one gives Renderer::render's pixel (the global FrameEngine),
+    and a reference-style engine T seeds the call with two of its draws --
+    the bits of a FrameEngine with that seed -- and successive calls advance
+    it (fresh streams, as the reference's shared engine gives)."""
     W, H, spp, depth = 24, 16, 4, 8
     out = str(tmp_path / "tp.bin")
     r = subprocess.run([facade_bin, "tracepixel", str(W), str(H), str(spp), str(depth), out],
