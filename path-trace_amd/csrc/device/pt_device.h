@@ -705,6 +705,12 @@ struct Sph
         init(s, c, q, e);
         ps.t0[PRIM] = s.t0, ps.t1[PRIM] = s.t1, ps.live[PRIM] = s.live;
     }
+    /* init() from the span span() already computed (the same values) */
+    template <class PS>
+    __device__ static __forceinline__ void init_ps(St &s, const PS &ps)
+    {
+        s.t0 = ps.t0[PRIM], s.t1 = ps.t1[PRIM], s.live = ps.live[PRIM];
+    }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { f(IC<PRIM>(), IC<MAT>()); }
     /* the same for primitives whose material SEL selects, all primitives not just positive ones */
@@ -839,6 +845,12 @@ struct Pln
         init(s, c, q, e);
         ps.t0[PRIM] = s.t0, ps.t1[PRIM] = s.t1, ps.live[PRIM] = s.live;
     }
+    /* init() from the span span() already computed (the same values) */
+    template <class PS>
+    __device__ static __forceinline__ void init_ps(St &s, const PS &ps)
+    {
+        s.t0 = ps.t0[PRIM], s.t1 = ps.t1[PRIM], s.live = ps.live[PRIM];
+    }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { f(IC<PRIM>(), IC<MAT>()); }
     /* the same for primitives whose material SEL selects, all primitives not just positive ones */
@@ -944,6 +956,14 @@ struct Pln
     {                                                                                               \
         A::span(ps, c.a, q, e);                                                                     \
         B::span(ps, c.b, q, e);                                                                     \
+    }                                                                                               \
+    template <class PS>                                                                             \
+    __device__ static __forceinline__ void init_ps(St &s, const PS &ps)                            \
+    {                                                                                               \
+        A::init_ps(s.a, ps);                                                                        \
+        B::init_ps(s.b, ps);                                                                        \
+        s.ea = !A::pull(s.a, s.sa);                                                                 \
+        s.eb = !B::pull(s.b, s.sb);                                                                 \
     }                                                                                               \
     template <class SEL, class PS>                                                                  \
     __device__ static __forceinline__ void span_sel(PS &ps, const Ctx &c, const Ray &q, const Env &e) \
@@ -1292,6 +1312,8 @@ struct Xf
     {
         C::span(ps, c.c, mkray(m_lin(e.P + MOFF, q.d)), e);
     }
+    template <class PS>
+    __device__ static __forceinline__ void init_ps(St &s, const PS &ps) { C::init_ps(s, ps); }
     template <class F>
     __device__ static __forceinline__ void each_pos(F &&f) { C::each_pos(f); }
     template <class SEL, class PS>
@@ -1357,6 +1379,32 @@ __device__ __forceinline__ bool first_hit(const typename R::Ctx &ctx, V3 d, cons
     return false;
 }
 
+/* The same lazy merge started from the primitive spans the fast checks just
+ * computed (init_ps: the values init() would compute): the primitive contexts
+ * are dead by then and the spans are not computed twice. */
+template <class R, class PS>
+__device__ __forceinline__ bool first_hit_ps(const PS &ps, float &t, u32 &ref, bool &exit_hit)
+{
+    typename R::St st;
+    R::init_ps(st, ps);
+    CS s;
+    while (R::pull(st, s)) {
+        if (s.t0 >= MAXV)
+            return false;
+        if (s.t0 >= EPS) {
+            t = s.t0, ref = s.r0, exit_hit = false;
+            return true;
+        }
+        if (s.t1 >= MAXV)
+            return false;
+        if (s.t1 >= EPS) {
+            t = s.t1, ref = s.r1, exit_hit = true;
+            return true;
+        }
+    }
+    return false;
+}
+
 /* First hit from every primitive's span at once, where the fast checks hold
  * (the union rule in union-only trees, else the pairwise checks): the hit is
  * then a positive primitive's own boundary -- its start (entry) if that is
@@ -1402,6 +1450,10 @@ __device__ __forceinline__ int span_first_hit(const PS &ps, bool &hit, float &t,
     return fok;
 }
 
+/* Spine and lane queries start the lazy merge from the spans they computed */
+#ifndef PT_MERGE_FROM_SPANS
+#define PT_MERGE_FROM_SPANS 1
+#endif
 /* The spine's query (one ray, the same on every lane): span_first_hit where
  * the checks hold, else the lazy merge.  The checks are wave-uniform here. */
 template <class R>
@@ -1416,7 +1468,12 @@ __device__ __forceinline__ bool spine_first_hit(const typename R::Ctx &ctx, V3 d
     if (!wave_any(!fok))
         return hit;
     merged = 1;
+#if PT_MERGE_FROM_SPANS
+    (void)ctx, (void)d, (void)e;
+    return first_hit_ps<R>(ps, t, ref, exit_hit);
+#else
     return first_hit<R>(ctx, d, e, t, ref, exit_hit);
+#endif
 }
 
 /* A lane's own query (camera rays, lane-finished mirror children): the same,
@@ -1432,7 +1489,11 @@ __device__ __forceinline__ bool lane_first_hit(const typename R::Ctx &ctx, V3 d,
     const int fok = span_first_hit<R>(ps, hit, t, ref, exit_hit);
     if (wave_any(!fok)) {
         if (!fok)
+#if PT_MERGE_FROM_SPANS
+            hit = first_hit_ps<R>(ps, t, ref, exit_hit);
+#else
             hit = first_hit<R>(ctx, d, e, t, ref, exit_hit);
+#endif
     }
     return hit;
 #else
