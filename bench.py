@@ -147,13 +147,25 @@ def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps, within=None):
            "host_cpus": os.cpu_count(), "affinity_cpus": host,
            "sample": "%d hashed pixels x %d spp of the same frame (%.1f s)" % (npix, spp, secs),
            "sample_queries_per_sample": round(qps, 2)}
+    scal = None
+    try:  # the measured thread scaling of this baseline (tools/cpu_scaling.py on a GPU box)
+        with open(os.path.join(ROOT, "profiles", "round5", "cpu_scaling.json")) as f:
+            rows = json.load(f)["C3_sample_scaling"]["rows"]
+        scal = {"threads": [r["threads"] for r in rows],
+                "parallel_efficiency": [round(r["parallel_efficiency"], 3) for r in rows],
+                "file": "profiles/round5/cpu_scaling.json"}
+    except (OSError, ValueError, KeyError):
+        pass
+    if scal:
+        out["thread_scaling_measured"] = scal
     if host > threads:
         # the reference pool spawns hardware_concurrency() threads (src/test.cpp:204); the
         # GPU box asks for its per-GPU CPU share only, so the whole host is a projection
-        # (pixels are independent: the pool scales linearly until memory bandwidth binds)
+        # (pixels are independent: linear is an upper bound -- the measured 8 -> 16 step
+        # is below it, thread_scaling_measured)
         out["all_host_cpus_projected"] = {
             "value": round(value * host / threads, 5), "cores": host,
-            "how": "linear from the measured %d threads (not measured)" % threads,
+            "how": "linear from the measured %d threads (not measured; an upper bound)" % threads,
             "why_not_measured": "the GPU box gives each GPU job a %d-thread CPU share (OMP_NUM_THREADS); the "
                                 "reference pool's hardware_concurrency() threads (src/test.cpp:204) would take the "
                                 "other GPUs' shares of this %d-CPU host" % (threads, host)}
