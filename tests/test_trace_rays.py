@@ -81,6 +81,20 @@ def test_gpu_trace_rays_fast_order_matches_oracle(name, builder, opts, tmp_path)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+# textured scenes (image, skybox, mirror-ball, spherical and log textures) in the ray-list module
+TEX_CASES = [("texture_zoo", 5), ("texture_transc_zoo", 5)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("builder,depth", TEX_CASES)
+def test_gpu_trace_rays_textures_match_oracle(builder, depth, tmp_path):
+    rays = T.trace_rays_input(256, seed=23)
+    root = T.build(builder)
+    got = pt.trace_rays(root, rays, depth, spp=2, order="fast")
+    want = O.trace_rays(to_text(root, str(tmp_path)), rays, 2, depth, order=O.ORDER_FAST)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
 @pytest.mark.gpu
 def test_gpu_trace_rays_block_path(tmp_path):
     """96 samples per ray: the slot-major launch with 32-sample block partials."""
