@@ -785,6 +785,9 @@ struct Sph
 #ifndef PT_PLANE_AXIS_DARK
 #define PT_PLANE_AXIS_DARK 1
 #endif
+#ifndef PT_PLANE_AXIS_DIV
+#define PT_PLANE_AXIS_DIV 1 /* an axis-aligned plane's d.n as one product */
+#endif
 /* AX >= 0: the normal has one nonzero component, axis AX >> 1, negative if
  * AX & 1 (codegen knows the scene's numbers); -1 otherwise. */
 template <int PRIM, int OFF, int MAT, int AX = -1>
@@ -814,7 +817,19 @@ struct Pln
     }
     __device__ static __forceinline__ void init(St &s, const Ctx &c, const Ray &q, const Env &e)
     {
-        const float div = dot(q.d, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+        float div;
+        if constexpr (AX >= 0 && PT_PLANE_AXIS_DIV) {
+            /* one nonzero component: (d.x n.x + d.y n.y) + d.z n.z is that
+             * component's product plus signed zeros -- the product itself
+             * whenever it is nonzero, and a zero either way when it is zero
+             * (which makes the plane degenerate, |div| < eps^2, regardless of
+             * its sign).  Directions are finite (camera rays, normalised
+             * children, reflections of them). */
+            const float dc = (AX >> 1) == 0 ? q.d.x : (AX >> 1) == 1 ? q.d.y : q.d.z;
+            div = dc * e.P[OFF + (AX >> 1)];
+        } else {
+            div = dot(q.d, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
+        }
         const bool small = __builtin_fabsf(div) < EPS * EPS;
         float t = div_core(c.num, mkrcp(div));
         const bool bad = !small && !(den_ok(div) && num_ok(c.num));
