@@ -273,6 +273,13 @@ int pt_scene_set_lane_walk(pt_scene *s, int frames);
  * dozen leaves each); supersedes pt_scene_set_lane_walk.  Takes effect at the
  * next compile/render. */
 int pt_scene_set_lane_scatter(pt_scene *s, int on);
+/* MI355X tuning knob, no reference counterpart: lane-walk scenes render in
+ * split launches (default on) -- a light kernel (no lazy merges, no wave walk,
+ * higher occupancy) over every chunk, then the full kernel over the chunks
+ * with a lane it could not finish.  A chunk's sums come from one kernel, so
+ * the bits are the same either way.  0 = every chunk through the full kernel.
+ * Takes effect at the next render. */
+int pt_scene_set_split(pt_scene *s, int on);
 /* Key of the code object for this scene/depth: a hash of the generated source,
  * the compiler options and the hiprtc version -- the file name of its entry in
  * the code-object cache (hex string, thread-local storage). */

@@ -84,6 +84,11 @@ struct PtLaunch
     long long ray0;     /* PT_RAYS: engine key index of slot 0 (slot k: ray0 + k) */
     int grab;           /* chunks a wave takes per work-queue atomic while plenty are
                            left (1 near the end of the launch); >= 1               */
+    const unsigned *list; /* split launches (lane-walk scenes): the full kernel takes its
+                           chunks from this list, stats[35] long (nullptr: every
+                           chunk of the launch)                                   */
+    unsigned *bail;     /* split launches: the light kernel appends the chunks it
+                           leaves to the full kernel here (count: stats[35])      */
 };
 /* The engine key index of a slot's item: its pixel index, or in a ray-list
  * module the caller's ray index */
@@ -1491,6 +1496,10 @@ __device__ __forceinline__ bool spine_first_hit(const typename R::Ctx &ctx, V3 d
 #endif
 }
 
+#ifdef PT_BAIL_STATS /* diagnostic builds: which chunks a merge-free kernel could finish */
+__device__ unsigned pt_bail_flag[1 << 20];
+__device__ __forceinline__ void pt_bail_mark() { pt_bail_flag[blockIdx.x * blockDim.x + threadIdx.x] = 1u; }
+#endif
 /* A lane's own query (camera rays, lane-finished mirror children): the same,
  * the lazy merge only on the lanes whose checks fail. */
 template <class R>
@@ -1503,6 +1512,10 @@ __device__ __forceinline__ bool lane_first_hit(const typename R::Ctx &ctx, V3 d,
     bool hit;
     const int fok = span_first_hit<R>(ps, hit, t, ref, exit_hit);
     if (wave_any(!fok)) {
+#ifdef PT_BAIL_STATS
+        if (!fok)
+            pt_bail_mark();
+#endif
         if (!fok)
 #if PT_MERGE_FROM_SPANS
             hit = first_hit_ps<R>(ps, t, ref, exit_hit);
@@ -1514,6 +1527,20 @@ __device__ __forceinline__ bool lane_first_hit(const typename R::Ctx &ctx, V3 d,
 #else
     return first_hit<R>(ctx, d, e, t, ref, exit_hit);
 #endif
+}
+
+/* The light kernel's lane query (split launches): the fast checks alone.
+ * undecided = the checks failed on this lane, whose sample then goes to the
+ * full kernel with its whole chunk (t / ref are not valid then). */
+template <class R>
+__device__ __forceinline__ bool lane_first_hit_light(const typename R::Ctx &ctx, V3 d, const Env &e, float &t,
+                                                     u32 &ref, bool &exit_hit, bool &undecided)
+{
+    PrimSpans<R::HI> ps;
+    R::span(ps, ctx, mkray(d), e);
+    bool hit;
+    undecided = !span_first_hit<R>(ps, hit, t, ref, exit_hit);
+    return hit && !undecided;
 }
 
 /* Fast first hit over precomputed primitive spans; valid when R::fast_ok. */
@@ -3293,7 +3320,7 @@ struct WalkFrame
     float ms;          /* its strength */
     int mdep;          /* its depth */
 };
-template <class S>
+template <class S, bool LIGHT = false>
 __device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 o0, V3 d0, float str0, const CamHit &ch,
                                           V3 &res, int &nq, int &nsh)
 {
@@ -3334,7 +3361,17 @@ __device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 o0, V3 d0
             } else {
                 typename S::Root::Ctx ctx;
                 S::Root::prep_l(ctx, o, e);
-                found = lane_first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+                if constexpr (LIGHT) {
+                    /* a query the checks cannot decide: the full kernel's */
+                    bool und;
+                    found = lane_first_hit_light<typename S::Root>(ctx, d, e, t, ref, ex, und);
+                    if (und) {
+                        ok = false;
+                        continue;
+                    }
+                } else {
+                    found = lane_first_hit<typename S::Root>(ctx, d, e, t, ref, ex);
+                }
             }
             if (!found) {
                 r = mk(0, 0, 0);
@@ -3964,7 +4001,7 @@ __device__ constexpr int min_workgroups()
  * none are left.  Per-chunk cost varies by ~10^5 (sky pixels vs diffuse
  * pixels), so static assignment or one-chunk-per-wave launches leave most
  * SIMDs idle behind the slowest wave of each workgroup. */
-template <class S, int MAXD, bool STRICT>
+template <class S, int MAXD, bool STRICT, bool LIGHT = false>
 __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const PtImage *__restrict__ imgs,
                                              const u64 *__restrict__ jump, float *__restrict__ out,
                                              const int *__restrict__ pixels, u64 *__restrict__ stats,
@@ -4029,7 +4066,10 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave], LSUM_LDS ? lsbuf[wave] : nullptr};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
-    u64 *work = stats + 15; /* chunk counter, zeroed before every launch */
+    /* Split launches (lane-walk scenes, see pt_render_light): the full kernel
+     * serves the light kernel's list, with its own counter (stats[36]) */
+    u64 *work = stats + (lp.list ? 36 : 15); /* chunk counter, zeroed before every launch */
+    const long long n_idx = lp.list ? (long long)(u32)uni((int)(u32)stats[35]) : n_chunks;
     /* The queue is one device-scope counter of chunks.  A single address takes
      * on the order of 10^8 atomics per second across the 8 XCDs, which caps
      * scenes of cheap samples (C5: 64-sample chunks at ~85 M/s).  So a wave
@@ -4048,7 +4088,7 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     const int GRAB = lp.grab > 1 ? lp.grab : 1;
     int cheap = 0; /* the last run took under PT_GRAB_TICKS per chunk (unknown: single chunks) */
     auto want = [&](long long from) { /* run length of the next request, seen from chunk `from` */
-        return (GRAB > 1 && cheap && n_chunks - from > 8ll * GRAB * nwaves) ? GRAB : 1;
+        return (GRAB > 1 && cheap && n_idx - from > 8ll * GRAB * nwaves) ? GRAB : 1;
     };
     auto dequeue = [&](int k) {
         long long c = 0;
@@ -4068,6 +4108,10 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     };
     long long next = dequeue();
 #endif
+#ifdef PT_BAIL_STATS
+    pt_bail_flag[blockIdx.x * blockDim.x + threadIdx.x] = 0u;
+    u64 bs[6] = {0, 0, 0, 0, 0, 0};
+#endif
     for (;;) {
 #if PT_GRAB_RUNS
         if (left == 0) {
@@ -4080,19 +4124,20 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             next = dequeue(nk);
 #endif
         }
-        const long long chunk = run++;
+        const long long idx = run++;
         left--;
-        if (chunk >= n_chunks)
+        if (idx >= n_idx)
             break;
 #else
-        const long long chunk = uniform_chunk(next);
-        if (chunk >= n_chunks)
+        const long long idx = uniform_chunk(next);
+        if (idx >= n_idx)
             break;
 #if PT_DEQUEUE_PREFETCH
         /* the next chunk's dequeue is in flight while this one is traced */
         next = dequeue();
 #endif
 #endif
+        const long long chunk = lp.list ? uniform_chunk((long long)lp.list[idx]) : idx;
         const long long item0 = chunk * CH;
         PT_T0(tchunk);
         /* the chunk's camera queries, one per lane */
@@ -4123,6 +4168,15 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             S::Root::prep(ctx, o, e);
 #endif
             bool ex = false;
+#ifdef PT_LANE_WALK
+            if constexpr (LIGHT) {
+                bool und;
+                ch.hit = lane_first_hit_light<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex, und) ? 1 : 0;
+                ch.ex = ex ? 1 : 0;
+                ldone = !und && lane_walk<S, true>(e, lp.depth, o, d, str, ch, lres, lq, lsh) ? 1 : 0;
+            } else
+#endif
+            {
             ch.hit = lane_first_hit<typename S::Root>(ctx, d, e, ch.t, ch.ref, ex) ? 1 : 0;
             ch.ex = ex ? 1 : 0;
 #if defined(PT_LANE_SCATTER) /* per scene, pt_scene_set_lane_scatter */
@@ -4132,9 +4186,28 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
 #else
             ldone = lane_sample<S>(e, lp.depth, o, d, str, ch, lres, lq, lsh) ? 1 : 0;
 #endif
+            }
         }
         PT_ACC2(cnt, 1, tchunk); /* the lane-parallel front end */
+        /* the light kernel leaves a chunk with a lane it could not finish (a
+         * query its checks cannot decide, a scatter loop, a deep tree) to the
+         * full kernel, whole: a chunk's sums come from one kernel */
+        bool bailed = false;
+        if constexpr (LIGHT) {
+            bailed = __ballot(lvalid && !ldone) != 0ull;
+            if (bailed && lane == 0)
+                lp.bail[atomicAdd(&stats[35], 1ull)] = (unsigned)chunk;
+        }
+#ifdef PT_BAIL_STATS
         {
+            unsigned &fl = pt_bail_flag[blockIdx.x * blockDim.x + threadIdx.x];
+            const u64 BM = __ballot(fl != 0u), BW = __ballot(lvalid && !ldone);
+            fl = 0u;
+            bs[0]++, bs[1] += BM ? 1 : 0, bs[2] += BW ? 1 : 0, bs[3] += (BM | BW) ? 1 : 0;
+            bs[4] += __popcll(BM), bs[5] += __popcll(BW);
+        }
+#endif
+        if (!bailed) {
             /* statistics of the samples finished by their lane */
 #if defined(PT_LANE_WALK) || defined(PT_LANE_SCATTER)
             {
@@ -4152,6 +4225,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
             cnt.shaded += (u64)__popcll(SH);
 #endif
         }
+        V3 mine = lres;
+        if constexpr (!LIGHT) {
         /* park the lanes' state in LDS for the walks below */
         uint4 *const lb = lbuf[wave];
         const bool lwalk = lvalid && !ldone;
@@ -4173,7 +4248,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
                 lb[j] = make_uint4(__float_as_uint(c.x), __float_as_uint(c.y), __float_as_uint(c.z), 0u);
         }
         const uint4 mr = lb[lane];
-        const V3 mine = mk(__uint_as_float(mr.x), __uint_as_float(mr.y), __uint_as_float(mr.z));
+        mine = mk(__uint_as_float(mr.x), __uint_as_float(mr.y), __uint_as_float(mr.z));
+        }
         PT_T0(tout);
 #if PT_GRAB_RUNS
         if (left == 0) {
@@ -4187,7 +4263,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         next = dequeue();
 #endif
         const long long my = item0 + lane;
-        if (lp.block_sums) {
+        if (bailed) {
+            /* the full kernel writes this chunk */
+        } else if (lp.block_sums) {
             /* the chunk is one 32-sample block of one slot (slot-major, chunk
              * 32, nsamp % 32 == 0): its 32-leaf pairwise tree is the block
              * partial of the fast order's pixel sum.  Level w adds lane
@@ -4231,6 +4309,10 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
         atomicAdd(&stats[6], cnt.slow);
         atomicAdd(&stats[7], cnt.dark);
         atomicAdd(&stats[24], cnt.mid);
+#ifdef PT_BAIL_STATS /* chunks; with a lane merge; with wave walks; either; lanes merged; lanes walked */
+        for (int k = 0; k < 6; k++)
+            atomicAdd(&stats[16 + k], bs[k]);
+#endif
         const u64 t_end = __builtin_amdgcn_s_memrealtime();
         atomicMax(&stats[26], ~t_start); /* earliest start, complemented */
         atomicMax(&stats[27], t_end);    /* latest end */
@@ -4336,7 +4418,26 @@ __device__ __forceinline__ void tex_eval(const Env &e, const float *__restrict__
     const float *__restrict__ P, const ptd::PtImage *__restrict__ imgs, const u64 *__restrict__ jump,      \
         float *__restrict__ out, const int *__restrict__ pixels, u64 *__restrict__ stats, ptd::PtLaunch lp
 
+/* Lane-walk scenes (C5) also get a light kernel for split launches: the
+ * chunks whose every lane the lane walk finishes with decided queries (97 % of
+ * C5's) at PT_LIGHT_WG workgroups per CU -- no lazy merge, no wave walk, so
+ * few registers -- and the rest through the full kernel at its own
+ * occupancy.  Same statements on the chunks it finishes: the same bits. */
+#ifdef PT_LANE_WALK
+#ifndef PT_LIGHT_WG
+#define PT_LIGHT_WG 4
+#endif
+#define PT_DEFINE_LIGHT(SCENE, MAXD)                                                                        \
+    extern "C" __global__ __launch_bounds__(64 * PT_WPW, PT_LIGHT_WG) void pt_render_light(PT_RENDER_ARGS)  \
+    {                                                                                                       \
+        ptd::render_chunk<SCENE, MAXD, false, true>(P, imgs, jump, out, pixels, stats, lp);                \
+    }
+#else
+#define PT_DEFINE_LIGHT(SCENE, MAXD)
+#endif
+
 #define PT_DEFINE_KERNELS(SCENE, MAXD)                                                                      \
+    PT_DEFINE_LIGHT(SCENE, MAXD)                                                                            \
     extern "C" __global__ __launch_bounds__(64 * PT_WPW, PT_MIN_WG(SCENE, MAXD)) void pt_render_fast(PT_RENDER_ARGS) \
     {                                                                                                       \
         ptd::render_chunk<SCENE, MAXD, false>(P, imgs, jump, out, pixels, stats, lp);                      \

@@ -71,6 +71,7 @@ struct SceneImpl
     int fast_spine = 0;            /* spine queries try all spans + the fast checks first */
     int lane_walk = 0;             /* register frames of the per-lane scatter-free tree walk (0 = off) */
     int lane_scatter = 0;          /* per-lane walk of whole trees, scatter loops included */
+    int split = 1;                 /* lane-walk scenes: light kernel first (launch-time only) */
     std::map<int, std::unique_ptr<DeviceState>> devices;
     std::shared_ptr<struct QueryCache> qcache; /* loaded query modules (runtime.cpp) */
     std::string last_key;

@@ -76,6 +76,8 @@ struct PtLaunchHost /* must match ptd::PtLaunch */
     const float *rays;
     long long ray0;
     int grab;
+    const unsigned *list;
+    unsigned *bail;
 };
 
 template <class T>
@@ -115,8 +117,11 @@ struct DeviceState
     std::string key;
     hipModule_t mod = nullptr;
     hipFunction_t fast = nullptr, strict = nullptr, reduce = nullptr;
+    hipFunction_t light = nullptr; /* lane-walk modules: the split launch's light kernel */
     int wpw = 1; /* waves (chunks of 64 items) per workgroup, from the kernel's launch bounds */
     int resident_blocks = 0; /* persistent grid size: resident workgroups per CU x CUs */
+    int light_blocks = 0;    /* the same for the light kernel */
+    DevBuf<unsigned> bail;   /* the chunks the light kernel leaves to the full one */
     std::vector<float> params;
     DevBuf<float> P;
     DevBuf<PtImageDev> imgs;
@@ -470,6 +475,20 @@ DeviceState &device_state(SceneImpl &s, int device, const Generated &g, bool ray
         HIPCHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ds->fast, mt, 0));
         HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         ds->resident_blocks = std::max(1, per_cu) * std::max(1, cus);
+        /* lane-walk modules define pt_render_light (pt_device.h PT_DEFINE_LIGHT) */
+        ds->light = nullptr;
+        ds->light_blocks = 0;
+        if (hipModuleGetFunction(&ds->light, ds->mod, "pt_render_light") != hipSuccess) {
+            (void)hipGetLastError();
+            ds->light = nullptr;
+        } else {
+            int lt = 0;
+            HIPCHECK(hipFuncGetAttribute(&lt, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, ds->light));
+            if (lt != mt)
+                throw Error(PT_ERR_DEVICE, "light kernel block size differs from the megakernel's");
+            HIPCHECK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ds->light, mt, 0));
+            ds->light_blocks = std::max(1, per_cu) * std::max(1, cus);
+        }
         ds->key = g.key;
     }
     if (ds->params != g.params) {
@@ -588,6 +607,20 @@ long long slot_permutation(long long nslots)
         if (prime(m) && nslots % m != 0)
             return m;
     return 0;
+}
+
+/* split launches of lane-walk modules (pt_render_light + pt_render_fast);
+ * PT_SPLIT=0 is an experiment hook: every chunk through the full kernel */
+bool split_launches()
+{
+    static const bool on = [] {
+        const char *env = getenv("PT_SPLIT");
+        if (!env || !*env)
+            return true;
+        fprintf(stderr, "pt: experiment hook PT_SPLIT=%s active\n", env);
+        return atoi(env) != 0;
+    }();
+    return on;
 }
 
 /* Chunks a wave takes per work-queue atomic while its chunks are cheap and
@@ -820,6 +853,9 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             lp.rays = rays;
             lp.ray0 = ray0;
             lp.grab = grab_chunks(s);
+            /* split launch (lane-walk modules, fast order): the light kernel
+             * over every chunk, then the full kernel over the ones it left */
+            const bool split = ds.light && fn == ds.fast && s.split && split_launches() && chunks < (1ll << 32);
             reduce_mode = p->order == PT_ORDER_REFERENCE ? 0 : lp.block_sums ? 2 : 1;
             ds.stage.ensure((size_t)(lp.block_sums ? npix * (nsamp / 32) * 3 : npix * nsamp * 3));
             const float *Pp = ds.P.p;
@@ -833,6 +869,16 @@ void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream
             int e0 = (int)pr.evs.size();
             if (timed)
                 event();
+            if (split) {
+                ds.bail.ensure((size_t)chunks);
+                HIPCHECK(hipMemsetAsync(ds.stats.p + 35, 0, 16, stream)); /* list length, its queue */
+                lp.bail = ds.bail.p;
+                const long long lblocks = std::min<long long>(ds.light_blocks, (chunks + wpw - 1) / wpw);
+                HIPCHECK(hipModuleLaunchKernel(ds.light, (unsigned)lblocks, 1, 1, 64 * wpw, 1, 1, 0, stream, args,
+                                               nullptr));
+                lp.bail = nullptr;
+                lp.list = ds.bail.p;
+            }
             HIPCHECK(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 64 * wpw, 1, 1, 0, stream, args, nullptr));
             if (timed) {
                 event();
@@ -1309,6 +1355,14 @@ int pt_scene_set_lane_walk(pt_scene *s, int frames)
         if (frames < 0 || frames > 8)
             throw Error(PT_ERR_ARG, "lane walk frames must be in [0, 8]");
         S(s).lane_walk = frames;
+        return PT_OK;
+    });
+}
+
+int pt_scene_set_split(pt_scene *s, int on)
+{
+    return guard([&] {
+        S(s).split = on ? 1 : 0;
         return PT_OK;
     });
 }

@@ -39,7 +39,7 @@ class DeviceScene:
     constructors (one pt_* call per reference constructor)."""
 
     def __init__(self, root: Object, workgroups_per_cu: int = 0, fast_spine: bool = False, lane_walk: int = 0,
-                 lane_scatter: bool = False):
+                 lane_scatter: bool = False, split: bool = True):
         L = _lib.lib()
         self._h = L.pt_scene_create()
         if not self._h:
@@ -52,6 +52,8 @@ class DeviceScene:
             _lib.check(L.pt_scene_set_lane_walk(self._h, int(lane_walk)))
         if lane_scatter:
             _lib.check(L.pt_scene_set_lane_scatter(self._h, 1))
+        if not split:
+            _lib.check(L.pt_scene_set_split(self._h, 0))
         self._img = {}
         self._mat = {}
         self.root = root

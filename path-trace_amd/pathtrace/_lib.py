@@ -105,6 +105,7 @@ SIGNATURES = {
     "pt_scene_set_occupancy": (_I, [_P, _I]),
     "pt_scene_set_fast_spine": (_I, [_P, _I]),
     "pt_scene_set_lane_walk": (_I, [_P, _I]),
+    "pt_scene_set_split": (_I, [_P, _I]),
     "pt_scene_set_lane_scatter": (_I, [_P, _I]),
     "pt_scene_kernel_key": (ctypes.c_char_p, [_P, _I]),
     "pt_selftest_math": (_I, [_I, ctypes.c_uint64, ctypes.c_uint64, _P]),

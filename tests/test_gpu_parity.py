@@ -131,6 +131,31 @@ def test_lane_walk_c5_same_bits(built):
     assert_bits(imgs[1], imgs[0], "C5 lane walk vs wave walk")
 
 
+@pytest.mark.parametrize("spp", [2, 64])
+def test_split_launch_same_bits(built, spp):
+    """Split launches (pt_scene_set_split, on by default in lane-walk scenes):
+    the light kernel finishes the chunks whose lanes decide every query and
+    leaves the rest, whole, to the full kernel -- the same bits and the same
+    query counts as every chunk through the full kernel, on C5's hashed pixels
+    plus a disk on the glass ball (where the light kernel gives chunks back),
+    sample-major (2 spp) and block-staged (64 spp) launches."""
+    cfg = scenes.CONFIGS["C5"]
+    rng = np.random.default_rng(5)
+    pix = np.sort(rng.choice(cfg.width * cfg.height, 4096, replace=False)).astype(np.int32)
+    disk = (1080 + np.arange(-24, 24)[:, None]) * cfg.width + (2460 + np.arange(-24, 24)[None, :])
+    pix = np.unique(np.concatenate([pix, disk.ravel().astype(np.int32)]))
+    out = []
+    for split in (True, False):
+        ds = pt.DeviceScene(cfg.scene(), workgroups_per_cu=cfg.wg_per_cu, fast_spine=cfg.fast_spine,
+                            lane_walk=cfg.lane_walk, split=split)
+        out.append(pt.render(ds, cfg.width, cfg.height, spp, cfg.depth, screen=cfg.screen, pixels=pix, stats=True))
+    (a, sa), (b, sb) = out
+    assert_bits(a, b, "C5 split vs full-kernel launch")
+    for k in ("samples", "queries", "shaded"):
+        if k in sa:
+            assert sa[k] == sb[k], (k, sa[k], sb[k])
+
+
 # (builder, depth) of the poisoned-LDS test build (test_lds_poison_bitexact)
 POISON_CASES = [("scene_p1", 8), ("csg_zoo", 6)]
 
