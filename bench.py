@@ -221,6 +221,10 @@ def main():
                              screen=cfg.screen, subset=keep, order=args.order, device=local,
                              max_buffer_bytes=40 << 30, force_split=use_dist)
     kernel_key = ds.kernel_key(cfg.depth)
+    # lane-walk scenes render in split launches (runtime.cpp: pt_render_light over every chunk, then
+    # pt_render_fast over the chunks it left; PT_SPLIT=0 turns them off); one render = one "launch" here
+    split = cfg.lane_walk and args.order == "fast" and os.environ.get("PT_SPLIT", "1") != "0"
+    render_kernels = "pt_render_light + pt_render_fast" if split else "pt_render_fast"
     by_samples, mine = share.by_samples, share.pixels
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
     stream = torch.cuda.current_stream()
@@ -312,7 +316,7 @@ def main():
             out["roofline"] = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TOPS,
                                "unit": "TFLOP/s", "frac": round(achieved / VALU_PEAK_TOPS, 4),
                                "traffic": round(ev["hbm_bytes_per_launch"]) if ev else None,
-                               "kernel": "pt_render_fast", "kernel_key": kernel_key,
+                               "kernel": render_kernels, "kernel_key": kernel_key,
                                "avg_launch_ms": round(kernel_ms, 2), "ops_per_query": opq}
             if not ev:
                 out["roofline"]["traffic_note"] = why

@@ -1,5 +1,8 @@
-"""Summarise tools/pmc_bench.sh: the render kernel's VALU/SALU busy fractions
-and HBM traffic under the bench command, per launch and per sample.
+"""Summarise tools/pmc_bench.sh: the render kernels' VALU/SALU busy fractions
+and HBM traffic under the bench command, per launch and per sample.  A render
+is one pt_render_fast launch, or for lane-walk scenes a split launch
+(pt_render_light over every chunk, then pt_render_fast over the chunks it
+left): the counters of both kernels are summed, so "per launch" is per render.
 
 VALUBusy follows rocprof's derived metric: SQ_ACTIVE_INST_VALU (quad-cycles
 summed over waves) x 4 / SIMDs / GRBM_GUI_ACTIVE per XCD (GRBM is summed over
@@ -17,14 +20,18 @@ out = sys.argv[1]
 SIMDS, XCDS = 1024, 8
 
 
+RENDER_KERNELS = ("pt_render_fast", "pt_render_light")
+seen = set()
+
+
 def counters(name):
     agg = collections.defaultdict(float)
-    n = 0
     for f in glob.glob("%s/%s/**/*counter_collection.csv" % (out, name), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Kernel_Name"].startswith("pt_render_fast"):
+            k = r["Kernel_Name"].split("(")[0].strip()
+            if k in RENDER_KERNELS:
                 agg[r["Counter_Name"]] += float(r["Counter_Value"])
-                n += 1
+                seen.add(k)
     return agg
 
 
@@ -47,7 +54,7 @@ samples = b["value"] * 1e6 * b["ms_per_step"] * 1e-3 * b["steps"]
 kernel_s = b["roofline"]["avg_launch_ms"] * 1e-3 if "roofline" in b else None
 gui = busy["GRBM_GUI_ACTIVE"] / XCDS
 res = {
-    "kernel": "pt_render_fast", "kernel_key": b["kernel_key"], "workload": b["config"]["workload"],
+    "kernel": " + ".join(k for k in reversed(RENDER_KERNELS) if k in seen), "kernel_key": b["kernel_key"], "workload": b["config"]["workload"],
     "bench_value": b["value"], "avg_launch_ms": b["roofline"]["avg_launch_ms"],
     "valu_busy": busy["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / gui,
     # > 1 here: SQ_ACTIVE_INST_VALU is summed over waves, and several waves'
