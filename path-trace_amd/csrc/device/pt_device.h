@@ -437,6 +437,35 @@ __device__ __forceinline__ float dpp_partner(float v)
 {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
+/* Inclusive prefix sum of v over the wave's lanes (lane l: v_0 + .. + v_l),
+ * integer, so any association gives the same value: Hillis-Steele within each
+ * row of 16 (row_shr 1, 2, 4, 8; lanes shifted in from outside the row read
+ * 0), then row 0's total into rows 1 and 3 and row 1's running total into rows
+ * 2 and 3 (row_bcast:15 / :31; the other rows add the old value 0).  Needs all
+ * 64 lanes active. */
+template <int CTRL, int ROWS>
+__device__ __forceinline__ u32 dpp_u32(u32 v)
+{
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, true);
+}
+__device__ __forceinline__ u32 wave_incl_scan(u32 v)
+{
+    v += dpp_u32<0x111, 0xF>(v);
+    v += dpp_u32<0x112, 0xF>(v);
+    v += dpp_u32<0x114, 0xF>(v);
+    v += dpp_u32<0x118, 0xF>(v);
+    v += dpp_u32<0x142, 0xA>(v);
+    v += dpp_u32<0x143, 0xC>(v);
+    return v;
+}
+/* (v << 1) | this lane's bit of the uniform mask m: one v_addc (v + v + carry-in m) */
+__device__ __forceinline__ u32 shl_lane_bit(u32 v, u64 m)
+{
+    u32 r;
+    u64 co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(v), "s"(m));
+    return r;
+}
 /* v + src broadcast from the last lane of the row(s) below, on rows ROWS only;
  * the other rows add -0.0f, which leaves every value (and the sign of 0) */
 template <int CTRL, int ROWS>
@@ -2248,6 +2277,9 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 #ifndef PT_LM_CHAINS
 #define PT_LM_CHAINS 1 /* lane-major rounds: engine chains per lane (2: the halves interleaved) */
 #endif
+#ifndef PT_LM_BITS
+#define PT_LM_BITS 1 /* lane-major rounds: per-lane bit planes + one wave prefix sum (burst_t) */
+#endif
 
 #ifndef PT_PASS_PAIR_FALLBACK
 /* 0: in a burst's fast pass over a Difference-free tree, lanes the one-pass
@@ -2308,6 +2340,8 @@ static_assert(PT_KATT % 2 == 0, "deferred rounds evaluate attempts in pairs");
 static_assert(64 * PT_KATT < PT_JUMP_ENTRIES, "jump table too short for PT_KATT");
 /* lane-major rounds count a lane's trailing failures in 4 balloted bit planes */
 static_assert(PT_KATT <= 15, "a lane's trailing-failure count must fit 4 bits");
+/* PT_LM_BITS: a round's totals in 10-bit fields of one packed wave prefix sum */
+static_assert(64 * PT_KATT < 1024, "round totals must fit 10 bits");
 
 /* One rejection attempt of the scatter loop body (path-trace.h:141-158):
  * s0 is the engine state before the attempt's three draws (outputs of s1, s2, s3). */
@@ -2673,6 +2707,66 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 u64 jA, jG;
                 jread(J.j24, lane, jA, jG);
                 const u64 s_lane = jA * rng.st + jG;
+#if PT_LM_BITS
+                /* Per-lane bit planes, attempt k at bit KATT-1-k (one v_addc
+                 * each: v + v + the balloted bit): accepted, hemisphere-failed
+                 * and kept attempts.  The round's totals, each lane's count of
+                 * kept attempts in the lanes below and the trailing failures
+                 * then come from one wave prefix sum of the packed per-lane
+                 * counts, and each lane writes its own kept attempts' ring
+                 * entries in a loop over its set bits (as many trips as the
+                 * most kept attempts of one lane) -- no per-attempt slot
+                 * numbering or masked store block, and no kept-mask array in
+                 * scalar registers. */
+                u32 abits = 0u, fbits = 0u, kbits = 0u;
+                u64 sk = s_lane;
+#pragma unroll
+                for (int k = 0; k < PT_KATT; k += 2) {
+                    const Attempt2 ap = attempt2_chain<KR0>(sk, n, kR);
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
+                        u64 D = 0ull;
+                        if (RAW)
+                            D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
+                        abits = shl_lane_bit(abits, ap.A[h]);
+                        fbits = shl_lane_bit(fbits, ap.F[h]);
+                        kbits = shl_lane_bit(kbits, ap.A[h] & ~D);
+                    }
+                }
+                /* failures after the lane's last accepted attempt (the bits
+                 * below the lowest accepted one; none accepted: all of them) */
+                const u32 tfl = (u32)__popc(fbits & ((abits & (0u - abits)) - 1u));
+                /* packed per-lane counts: accepted | kept << 10 | trailing failures << 20
+                 * (each total <= 64 KATT < 1024) */
+                const u32 pk = (u32)__popc(abits) | ((u32)__popc(kbits) << 10) | (tfl << 20);
+                const u32 incl = wave_incl_scan(pk), excl = incl - pk;
+                const u32 tot = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+                ta = (int)(tot & 0x3FFu);
+                tk = (int)((tot >> 10) & 0x3FFu);
+                const u64 Aor = __ballot(abits != 0u);
+                if (Aor) {
+                    /* the trailing failures of lane L (the last with an accepted
+                     * attempt) and of every lane above it */
+                    const int L = 63 - __builtin_clzll(Aor);
+                    fails_lm = (int)(tot >> 20) - (int)((u32)__builtin_amdgcn_readlane((int)excl, L) >> 20);
+                } else {
+                    fails_lm = fails + (int)(tot >> 20);
+                }
+                /* ring entries, numbered in child order: this lane's kept
+                 * attempts follow those of the lanes below */
+                int slot = nkeep + (int)((excl >> 10) & 0x3FFu);
+                for (u32 kb = kbits; kb != 0u;) {
+                    const int c = __builtin_clz(kb);
+                    if (slot < slot_end) {
+                        float4 *r = &ring[slot & (PT_RCAP - 1)];
+                        __builtin_memcpy(r, &s_lane, 8);
+                        r->z = __int_as_float(c - (32 - PT_KATT)); /* attempt k of the lane */
+                    }
+                    slot++;
+                    kb ^= 0x80000000u >> c;
+                }
+#else
                 int tf = 0;
                 u64 Aor = 0ull, K[PT_KATT];
 #if PT_LM_CHAINS == 2
@@ -2762,6 +2856,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 for (int b = 0; b < 4; b++)
                     sf += __popcll(__ballot((tf >> b) & 1) & GE) << b;
                 fails_lm = Aor ? sf : fails + sf;
+#endif
             } else if (DEFERRED) {
                 /* pairs of attempts in packed f32 */
                 u64 sk = lane_state();
