@@ -1644,6 +1644,38 @@ __device__ __forceinline__ int cheap_ok(const PS &ps)
         return u & R::isect_empty(ps);
 }
 
+/* cheap_ok and fast_first_hit of a union-only tree in one pass over the
+ * spans (the same candidate / better / minimum chain serves both): where the
+ * union rule holds and a candidate exists its start b0 is >= EPS, so the hit
+ * is that primitive's entry at b0 unless b0 >= MAXV -- fast_first_hit's exit
+ * branch (b0 < EPS) cannot occur.  Returns the rule's verdict; hit / t / mat
+ * are valid where it holds. */
+#ifndef PT_UNION_FUSED
+#define PT_UNION_FUSED 1
+#endif
+template <class R, class PS>
+__device__ __forceinline__ int union_first_hit(const PS &ps, bool &hit, float &t, int &mat)
+{
+    static_assert(R::UNION_ONLY, "union_first_hit needs a union-only tree");
+    int found = 0, tie = 0, bad = 0, bm = 0;
+    float b0 = 0.0f;
+    R::each_pos([&](auto x, auto m) {
+        constexpr int X = decltype(x)::value;
+        const int live = ps.live[X];
+        const int cand = live & (ps.t1[X] >= EPS);
+        const int better = cand & ((!found) | (ps.t0[X] < b0));
+        tie = better ? 0 : (tie | (cand & (ps.t0[X] == b0)));
+        bad |= live & ((ps.t0[X] != ps.t0[X]) | (ps.t1[X] != ps.t1[X]));
+        b0 = better ? ps.t0[X] : b0;
+        bm = better ? decltype(m)::value : bm;
+        found |= cand;
+    });
+    mat = bm;
+    t = b0;
+    hit = found && b0 < MAXV;
+    return ((!found) | ((b0 >= EPS) & !tie)) & !bad;
+}
+
 /* ---- clear pass -------------------------------------
  * When every selected (emissive) primitive is reached from the root through
  * Union and TransformedObject nodes only (R::clear_ok), and on a lane every
@@ -3024,6 +3056,25 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
             S::Root::span(ps, ctx, mkray(dir), e);
             PT_MARK(10);
             int fok;
+#if PT_UNION_FUSED && !PT_PASS_PAIR_FALLBACK
+            if constexpr (S::Root::UNION_ONLY) {
+                bool fh;
+                float t;
+                int mat;
+                fok = union_first_hit<typename S::Root>(ps, fh, t, mat);
+                PT_MARK(11);
+                if (fok) {
+                    V3 col = mk(0, 0, 0);
+                    if (fh)
+                        col = S::emis(mat, hit + t * dir, e);
+                    PT_MARK(12);
+                    const V3 term = ((aN * en.w) * rc) * col;
+                    ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
+                    return true;
+                }
+                return false;
+            }
+#endif
             if constexpr (S::Root::NO_DIFF) {
                 /* the union rule over the positive primitives (and empty
                  * intersections); the pairwise checks only where it cannot
