@@ -234,6 +234,25 @@ __device__ __forceinline__ V3 cnormalize(V3 v) /* == normalize(v), bitwise */
     }
     return q;
 }
+/* normalize() of a kept attempt's direction in a diffuse burst (scatter
+ * coefficient 1: w = v, the unit-ball draw itself), where cnormalize's exact
+ * fast sequence needs none of its fallbacks: the hemisphere test passed, so
+ * n.w > EPS with |n| = 1 + O(2^-23) and |w|^2 >= 1e-6 > 2^-96 (sqrt_core_ok)
+ * and 1e-3 < |w| < 1.01 (den_ok, and m != 0); each component is a u11 value,
+ * +0 or of magnitude in [2^-24, 1] (num_ok, or a +0 numerator, whose quotient
+ * div_core also gets exactly: +0).  Same bits as normalize(). */
+#ifndef PT_KEPT_NORM
+#define PT_KEPT_NORM 1
+#endif
+__device__ __forceinline__ V3 cnormalize_kept(V3 v)
+{
+#if PT_KEPT_NORM
+    const Rcp R = mkrcp(sqrt_core(dot(v, v)));
+    return mk(div_core(v.x, R), div_core(v.y, R), div_core(v.z, R));
+#else
+    return cnormalize(v);
+#endif
+}
 /* normalize() where the device library needs it (normals, reflect / refract,
  * the spherical sky map): PT_FAST_NORM=1 takes the exact fast sequence (same
  * bits).  Off: same-box A/B (profiles/round5/ab_grab_fastnorm_c3_full.txt)
@@ -2312,6 +2331,9 @@ __device__ __forceinline__ void lds_put(LdsBox<T> &b, const T &t)
 #ifndef PT_LM_BITS
 #define PT_LM_BITS 1 /* lane-major rounds: per-lane bit planes + one wave prefix sum (burst_t) */
 #endif
+#ifndef PT_RING_FITS
+#define PT_RING_FITS 1 /* PT_LM_BITS: the ring writes of a round whose kept attempts all fit skip the slot test */
+#endif
 
 #ifndef PT_PASS_PAIR_FALLBACK
 /* 0: in a burst's fast pass over a Difference-free tree, lanes the one-pass
@@ -2788,16 +2810,26 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                 /* ring entries, numbered in child order: this lane's kept
                  * attempts follow those of the lanes below */
                 int slot = nkeep + (int)((excl >> 10) & 0x3FFu);
-                for (u32 kb = kbits; kb != 0u;) {
-                    const int c = __builtin_clz(kb);
-                    if (slot < slot_end) {
-                        float4 *r = &ring[slot & (PT_RCAP - 1)];
-                        __builtin_memcpy(r, &s_lane, 8);
-                        r->z = __int_as_float(c - (32 - PT_KATT)); /* attempt k of the lane */
+                auto put = [&](u32 kb, bool check) {
+                    for (; kb != 0u;) {
+                        const int c = __builtin_clz(kb);
+                        if (!check || slot < slot_end) {
+                            float4 *r = &ring[slot & (PT_RCAP - 1)];
+                            __builtin_memcpy(r, &s_lane, 8);
+                            r->z = __int_as_float(c - (32 - PT_KATT)); /* attempt k of the lane */
+                        }
+                        slot++;
+                        kb ^= 0x80000000u >> c;
                     }
-                    slot++;
-                    kb ^= 0x80000000u >> c;
-                }
+                };
+#if PT_RING_FITS
+                /* the common round: every kept attempt has a free slot (a
+                 * wave-uniform test once instead of a compare per entry) */
+                if (tk <= free_slots)
+                    put(kbits, false);
+                else
+#endif
+                    put(kbits, true);
 #else
                 int tf = 0;
                 u64 Aor = 0ull, K[PT_KATT];
@@ -3209,7 +3241,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         V3 w = mk(u11(s1.hi), u11(s2.hi), u11(s3.hi));
                         if (!KR0)
                             w = w + kR;
-                        const V3 nd = cnormalize(w);
+                        const V3 nd = KR0 ? cnormalize_kept(w) : cnormalize(w);
                         en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
                     }
                     if constexpr (CLEAR) {
