@@ -584,6 +584,19 @@ __device__ __forceinline__ Ray mkray(V3 d)
     q.aok = den_ok(q.a) ? 1 : 0;
     return q;
 }
+/* The same for a normalised direction (the burst passes' children): |d|^2 is
+ * 1 within 1e-6, so den_ok(a) holds and the spans' quotient checks fold */
+#ifndef PT_UNIT_RAY
+#define PT_UNIT_RAY 1
+#endif
+__device__ __forceinline__ Ray mkray_unit(V3 d)
+{
+    Ray q = mkray(d);
+#if PT_UNIT_RAY
+    q.aok = 1;
+#endif
+    return q;
+}
 
 /* ---- fast first-hit ----------------------------------
  * Every primitive contributes at most one span.  When every pair of spans that
@@ -3085,7 +3098,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 #endif
             PrimSpans<S::Root::HI> ps;
             PT_MARK(9);
-            S::Root::span(ps, ctx, mkray(dir), e);
+            S::Root::span(ps, ctx, mkray_unit(dir), e);
             PT_MARK(10);
             int fok;
 #if PT_UNION_FUSED && !PT_PASS_PAIR_FALLBACK
@@ -3242,7 +3255,9 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         if (!KR0)
                             w = w + kR;
                         const V3 nd = KR0 ? cnormalize_kept(w) : cnormalize(w);
-                        en = make_float4(nd.x, nd.y, nd.z, 1.0f - (1.0f - dot(nd, n)) * sc);
+                        /* KR0: sc == 1, and x * 1 == x */
+                        en = make_float4(nd.x, nd.y, nd.z,
+                                         KR0 ? 1.0f - (1.0f - dot(nd, n)) : 1.0f - (1.0f - dot(nd, n)) * sc);
                     }
                     if constexpr (CLEAR) {
                         park = 1;
@@ -3250,7 +3265,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                             PT_MARK(16);
                             const V3 dir = mk(en.x, en.y, en.z);
                             const typename S::Root::Ctx ctx = lds_get(*cxp);
-                            const Ray q = mkray(dir);
+                            const Ray q = mkray_unit(dir);
                             const u64 CM = S::Root::template clear_mask<Emissive<S>, true>(ctx, q, e);
                             PrimSpans<S::Root::HI> ps;
                             S::Root::template span_sel<Emissive<S>>(ps, ctx, q, e);
