@@ -33,6 +33,9 @@ struct Gen
     std::vector<int> images;
     int prim = 0, spheres = 0, planes = 0;
     int depth_guard = 0;
+    int xf_depth = 0;          /* TransformedObjects above the node being generated */
+    int unit_axis[3] = {0, 0, 0}; /* planes with normal +-e_k outside transforms */
+    std::vector<std::pair<size_t, int>> unit_planes; /* (position of the ",U" mark in a node string, axis) */
 
     explicit Gen(const SceneImpl &sc) : s(sc) {}
 
@@ -92,7 +95,17 @@ struct Gen
                 }
             if (nz != 1 || !std::isfinite(o.f[ax >> 1]))
                 ax = -1;
-            t << "Pln<" << prim++ << "," << off << "," << material(o.mat) << "," << ax << ">";
+            /* a unit axis normal outside transforms: the plane may share the
+             * ray's reciprocal of that direction component with the other
+             * such planes of its axis (marked here, decided once the whole
+             * tree is known: see shared_axes) */
+            const bool unit = ax >= 0 && xf_depth == 0 && std::fabs(o.f[ax >> 1]) == 1.0f;
+            t << "Pln<" << prim++ << "," << off << "," << material(o.mat) << "," << ax;
+            if (unit) {
+                unit_axis[ax >> 1]++;
+                t << "@" << (ax >> 1);
+            }
+            t << ">";
             planes++;
             break;
         }
@@ -110,13 +123,40 @@ struct Gen
             mat_inverse(o.f, inv); /* TransformedSpanIterator: inv(invert(m)), object.h:49-51 */
             int moff = put(o.f, 12);
             int ioff = put(inv, 12);
-            t << "Xf<" << moff << "," << ioff << "," << obj(o.a) << ">";
+            xf_depth++;
+            const std::string child = obj(o.a);
+            xf_depth--;
+            t << "Xf<" << moff << "," << ioff << "," << child << ">";
             break;
         }
         }
         if (prim >= (1 << 17))
             throw Error(PT_ERR_ARG, "too many primitives");
         return t.str();
+    }
+
+    /* The planes marked '@k' share the ray's reciprocal of component k when
+     * at least two of them lie on axis k: the mark becomes the Pln UNIT
+     * argument there and disappears elsewhere; mask = the shared axes
+     * (PT_AXIS_SHARE). */
+    std::string shared_axes(const std::string &t, int &mask) const
+    {
+        mask = 0;
+        for (int k = 0; k < 3; k++)
+            if (unit_axis[k] >= 2)
+                mask |= 1 << k;
+        std::string r;
+        r.reserve(t.size());
+        for (size_t i = 0; i < t.size(); i++) {
+            if (t[i] == '@' && i + 1 < t.size()) {
+                if ((mask >> (t[i + 1] - '0')) & 1)
+                    r += ",1";
+                i++;
+            } else {
+                r += t[i];
+            }
+        }
+        return r;
     }
 
     std::string tex(int id)
@@ -182,7 +222,8 @@ Generated generate(const SceneImpl &s, int depth, bool rays)
     if (s.root < 0)
         throw Error(PT_ERR_ARG, "scene has no root object (pt_set_root)");
     Gen g(s);
-    std::string root = g.obj(s.root);
+    int axis_share = 0;
+    const std::string root = g.shared_axes(g.obj(s.root), axis_share);
 
     /* material dispatchers; texture params are appended after geometry */
     struct MatTypes
@@ -258,6 +299,9 @@ Generated generate(const SceneImpl &s, int depth, bool rays)
     /* ... and run generation rounds of 6 attempts per lane (C2 +1.7 % over 8,
      * 4 of 4 reps on one box, profiles/round4/ab_katt_c2_fixed.txt; 4: -0.9 %;
      * C3 lost 9 % at 6 in round 3) */
+    /* axes whose unit-normal planes share the ray's reciprocal (Pln UNIT) */
+    if (axis_share)
+        src << "#define PT_AXIS_SHARE " << axis_share << "\n";
     if (root.find("Diff<") == std::string::npos)
         src << "#ifndef PT_SPHERE_SKIP\n#define PT_SPHERE_SKIP 1\n#endif\n"
             << "#ifndef PT_KATT\n#define PT_KATT 6\n#endif\n";
@@ -349,10 +393,14 @@ Generated generate_query(const SceneImpl &s, int obj, int tex)
 {
     Gen g(s);
     std::ostringstream src;
+    int axis_share = 0;
+    const std::string qroot = obj >= 0 ? g.shared_axes(g.obj(obj), axis_share) : std::string();
+    if (axis_share)
+        src << "#define PT_AXIS_SHARE " << axis_share << "\n";
     src << device_library_source() << "\n";
     src << "namespace ptgen {\nusing namespace ptd;\n";
     if (obj >= 0)
-        src << "typedef " << g.obj(obj) << " QRoot;\n";
+        src << "typedef " << qroot << " QRoot;\n";
     if (tex >= 0)
         src << "typedef " << g.tex(tex) << " QTex;\n";
     src << "} // namespace ptgen\n";

@@ -568,12 +568,21 @@ __device__ __forceinline__ void start_from_start(CS &a, const CS &b) { a.t0 = b.
 
 /* One query direction as every primitive of a traversal sees it: |d|^2 and
  * its refined reciprocal are shared (the sphere quotients all divide by a). */
+#ifdef PT_NO_AXIS_SHARE /* A/B hook: every plane takes its own reciprocal */
+#undef PT_AXIS_SHARE
+#endif
 struct Ray
 {
     V3 d;
     float a;
     Rcp ra;
     int aok; /* den_ok(a) */
+#ifdef PT_AXIS_SHARE
+    /* direction components k of PT_AXIS_SHARE: their refined reciprocals and
+     * den_ok, shared by the unit-normal planes of axis k (Pln UNIT) */
+    Rcp rk[3];
+    int rkok[3];
+#endif
 };
 __device__ __forceinline__ Ray mkray(V3 d)
 {
@@ -582,6 +591,15 @@ __device__ __forceinline__ Ray mkray(V3 d)
     q.a = dot(d, d);
     q.ra = mkrcp(q.a);
     q.aok = den_ok(q.a) ? 1 : 0;
+#ifdef PT_AXIS_SHARE
+    const float dk[3] = {d.x, d.y, d.z};
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        if ((PT_AXIS_SHARE >> k) & 1) {
+            q.rk[k] = mkrcp(dk[k]);
+            q.rkok[k] = den_ok(dk[k]) ? 1 : 0;
+        }
+#endif
     return q;
 }
 /* The same for a normalised direction (the burst passes' children): |d|^2 is
@@ -856,7 +874,11 @@ struct Sph
 #endif
 /* AX >= 0: the normal has one nonzero component, axis AX >> 1, negative if
  * AX & 1 (codegen knows the scene's numbers); -1 otherwise. */
-template <int PRIM, int OFF, int MAT, int AX = -1>
+/* UNIT: the normal is +-e_(AX >> 1) exactly and the scene has another such
+ * plane on that axis (codegen PT_AXIS_SHARE): div = +-d_k, and the quotient
+ * num / div is +-(num / d_k) -- IEEE division is sign-symmetric -- taken
+ * with the ray's shared reciprocal of d_k. */
+template <int PRIM, int OFF, int MAT, int AX = -1, int UNIT = 0>
 struct Pln
 {
     static constexpr int LO = PRIM, HI = PRIM + 1;
@@ -897,8 +919,20 @@ struct Pln
             div = dot(q.d, mk(e.P[OFF], e.P[OFF + 1], e.P[OFF + 2]));
         }
         const bool small = __builtin_fabsf(div) < EPS * EPS;
-        float t = div_core(c.num, mkrcp(div));
-        const bool bad = !small && !(den_ok(div) && num_ok(c.num));
+        float t;
+        bool bad;
+#ifdef PT_AXIS_SHARE
+        if constexpr (UNIT != 0 && AX >= 0) {
+            /* e.P[OFF + k] is +-1: div == +-d_k exactly, |div| == |d_k| */
+            const float q0 = div_core(c.num, q.rk[AX >> 1]);
+            t = (AX & 1) ? -q0 : q0;
+            bad = !small && !(q.rkok[AX >> 1] && num_ok(c.num));
+        } else
+#endif
+        {
+            t = div_core(c.num, mkrcp(div));
+            bad = !small && !(den_ok(div) && num_ok(c.num));
+        }
         if (wave_any(bad)) {
         PT_COLD();
             if (bad)
