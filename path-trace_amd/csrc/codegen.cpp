@@ -309,6 +309,13 @@ Generated generate(const SceneImpl &s, int depth, bool rays)
      * (+1.1 %, 3 of 3 reps, profiles/round4/ab_katt_c3.txt; 6: -5.4 %) */
     else if (s.lane_walk == 0 && !s.lane_scatter)
         src << "#ifndef PT_KATT\n#define PT_KATT 10\n#endif\n";
+    /* ... and are scheduled by the iterative max-occupancy strategy (same-box
+     * A/B at 1 024 spp: C3 +0.3 %, 4 of 4 reps; C5 -2.6 %, C2 -0.4 %,
+     * profiles/round5/ab_sched_maxocc.txt); not when the PT_JIT_OPTIONS hook
+     * names a strategy of its own (an LLVM option may occur once) */
+    const char *jit_opts = getenv("PT_JIT_OPTIONS");
+    const bool maxocc = root.find("Diff<") != std::string::npos && s.lane_walk == 0 && !s.lane_scatter &&
+                        !(jit_opts && strstr(jit_opts, "sched-strategy"));
     /* experiment hook: A/B a different device library text in the same run,
      * e.g. PT_DEVICE_HEADER=tools/ab/old.h (profiling only) */
     if (const char *hdr = getenv("PT_DEVICE_HEADER")) {
@@ -378,6 +385,8 @@ Generated generate(const SceneImpl &s, int depth, bool rays)
         out.params.push_back(0.0f);
     out.image_ids = g.images;
     out.maxd = maxd;
+    if (maxocc)
+        out.options = {"-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"};
     out.n_prims = g.prim;
     out.n_spheres = g.spheres;
     out.n_planes = g.planes;

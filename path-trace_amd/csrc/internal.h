@@ -94,6 +94,7 @@ struct Generated
     std::vector<int> mat_ids;   /* compact material index -> scene material index     */
     int maxd = 0;
     int n_prims = 0, n_spheres = 0, n_planes = 0, n_mats = 0;
+    std::vector<std::string> options; /* per-scene compiler options (part of the code-object key) */
 };
 
 /* rays: the module of pt_trace_rays (PT_RAYS), whose items are caller rays */

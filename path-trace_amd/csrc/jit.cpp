@@ -148,6 +148,7 @@ std::string full_key(const Generated &g)
     std::ostringstream k;
     k << g.source << "\n";
     for (const char *o : kOptions) k << o << "\n";
+    for (const std::string &o : g.options) k << o << "\n";
     for (const std::string &o : extra_options()) k << o << "\n";
     k << "hiprtc " << maj << "." << min << "\n";
     uint64_t h = 1469598103934665603ull;
@@ -170,6 +171,8 @@ std::vector<char> compile(const Generated &g, std::string &log)
     if (R.create(&prog, g.source.c_str(), "pt_scene.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         throw Error(PT_ERR_COMPILE, "hiprtcCreateProgram failed");
     std::vector<const char *> opts(std::begin(kOptions), std::end(kOptions));
+    for (const std::string &o : g.options)
+        opts.push_back(o.c_str());
     const std::vector<std::string> extra = extra_options();
     for (const std::string &o : extra)
         opts.push_back(o.c_str());
