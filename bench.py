@@ -6,14 +6,23 @@ reference CPU renderer on a hashed pixel subset.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU)
 
+Launch.  Without torchrun (no WORLD_SIZE in the environment) and --gpus N > 1,
+this process starts N rank processes itself (a torch.distributed.run child on
+127.0.0.1) and exits with their status; it decides that before any GPU call and
+never runs a rank itself.  Under torchrun WORLD_SIZE must equal --gpus, and
+over RCCL --gpus may not exceed the visible GPUs: either mismatch exits
+non-zero, never falling back to fewer ranks.
+
 One step = one full frame.  N = 1: the HIP megakernel (libpt.so, C ABI)
-renders every pixel into a device frame buffer.  N > 1 (--split samples, the
-default): every rank renders every pixel for its share of the samples
-(sample_begin / sum_only), the per-pixel sums are reduced to rank 0 over RCCL
-and divided by spp; --split tiles: every rank renders the hashed 16x16 tiles
-it owns (pathtrace.dist) and the disjoint frames are sum-reduced.  The timed
-region is bracketed by barrier + device synchronise and the max over ranks is
-reported.  Inputs (the scene) are resident before timing.
+renders every pixel into a device frame buffer.  N > 1 (--split tiles, the
+default): every rank renders the 4x4 tiles it owns in the lattice deal
+(pathtrace.dist: any N consecutive tiles of a row go to N different ranks),
+and the disjoint frames are sum-reduced to rank 0 over RCCL -- bit-identical to
+the one-GPU frame; --split samples: every rank renders every pixel for its
+share of the samples (sample_begin / sum_only), the per-pixel sums are reduced
+and divided by spp.  The timed region is bracketed by barrier + device
+synchronise and the max over ranks is reported.  Inputs (the scene) are
+resident before timing.
 
 Extra fields: `roofline` (VALU-bound: the SURVEY.md s8(d) FP32 op model per
 root query x the kernel's exact query count / HIP-event kernel time, against
@@ -95,11 +104,102 @@ def parse():
     ap.add_argument("--force-dist", action="store_true",
                     help="take the N > 1 step at any world size: torch.distributed over RCCL (a one-rank group "
                          "when launched without torchrun), per-pixel sums, the device reduce, rank 0's division")
-    ap.add_argument("--split", choices=["samples", "tiles"], default="samples",
-                    help="N>1: each rank renders every pixel for its share of the samples (balanced to noise), "
-                         "or the hashed 16x16 tiles it owns (bit-identical to 1 GPU, measured 1.19 max/mean "
-                         "shard imbalance on C4)")
+    ap.add_argument("--split", choices=["samples", "tiles"], default="tiles",
+                    help="N>1: each rank renders the tiles it owns (bit-identical to 1 GPU), or every pixel for "
+                         "its share of the samples (per-pixel sums, ~1e-7 relative reassociation)")
+    ap.add_argument("--deal", choices=["lattice", "hashed"], default="lattice",
+                    help="--split tiles: tile (tx, ty) -> rank (tx + 3 ty) mod N, or round-robin in hashed order")
+    ap.add_argument("--tile", type=int, default=0, help="tile edge in pixels (0 = the deal's default: 4 / 16)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and rank plumbing only (process group, barrier, max over ranks, rank 0's line) "
+                         "with no render: prints a line with value null and dry_run true")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def visible_gpus() -> int:
+    """GPUs this process could use (torch.cuda.device_count does not initialise HIP)."""
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+def launch_check(args):
+    """Decide, before any GPU call, whether this process is a rank or the
+    launcher of --gpus ranks.  Returns None for a rank, else an exit status."""
+    env_world = os.environ.get("WORLD_SIZE")
+    need_gpus = not args.dry_run and args.backend == "nccl"
+    if env_world is not None:  # launched by torch.distributed.run (the driver's N > 1 form, or ours)
+        if int(env_world) != args.gpus:
+            print("bench.py: WORLD_SIZE=%s but --gpus %d: refusing to report a %s-rank run as %d GPUs" % (
+                env_world, args.gpus, env_world, args.gpus), file=sys.stderr)
+            return 2
+        if need_gpus and int(os.environ.get("LOCAL_RANK", "0")) >= visible_gpus():
+            print("bench.py: LOCAL_RANK %s has no GPU (%d visible)" % (os.environ.get("LOCAL_RANK"),
+                                                                      visible_gpus()), file=sys.stderr)
+            return 2
+        return None
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if need_gpus and args.gpus > visible_gpus():
+        print("bench.py: --gpus %d but %d GPU(s) visible" % (args.gpus, visible_gpus()), file=sys.stderr)
+        return 2
+    if args.gpus == 1:
+        return None
+    # N > 1 without torchrun: start N ranks (fresh processes: this one has not touched the GPU)
+    env = dict(os.environ)
+    if "OMP_NUM_THREADS" not in env:  # torchrun would pin it to 1 and starve rank 0's CPU leg
+        env["OMP_NUM_THREADS"] = str(len(os.sched_getaffinity(0)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+def _atoi(text: str) -> int:
+    """C atoi: leading blanks, an optional sign, the leading digits; 0 if none"""
+    import re
+    m = re.match(r"\s*([+-]?\d+)", text)
+    return int(m.group(1)) if m else 0
+
+
+def split_launches_env() -> bool:
+    """the runtime's split_launches() (runtime.cpp): PT_SPLIT unset or empty = on, else atoi != 0"""
+    v = os.environ.get("PT_SPLIT", "")
+    return True if not v else _atoi(v) != 0
+
+
+def dry_run(args):
+    """--dry-run: the rank plumbing of main() without the GPU (CPU tests of the launcher)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if "MASTER_ADDR" not in os.environ:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("gloo")
+    dist.barrier()
+    t0 = time.perf_counter()
+    dist.barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    ranks = torch.tensor([1.0])
+    dist.all_reduce(ranks, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        print(json.dumps({"metric": "Msamples/sec at 1920x1080x1024spp; per-channel RMSE vs CPU ref",
+                          "value": None, "dry_run": True, "n_gpus": world, "ranks_joined": int(ranks[0]),
+                          "steps": args.steps, "warmup": args.warmup, "split": args.split, "deal": args.deal}),
+              flush=True)
+    dist.destroy_process_group()
 
 
 def cpu_threads(requested: int) -> int:
@@ -177,6 +277,12 @@ def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps, within=None):
 
 def main():
     args = parse()
+    status = launch_check(args)
+    if status is not None:
+        sys.exit(status)
+    if args.dry_run:
+        dry_run(args)
+        return
     import torch
     import pathtrace as pt
     from pathtrace import dist as ptdist
@@ -194,11 +300,7 @@ def main():
     if use_dist:
         import torch.distributed as dist
         if "MASTER_ADDR" not in os.environ:  # --force-dist without torchrun: a one-rank group
-            import socket
-            with socket.socket() as sk:
-                sk.bind(("127.0.0.1", 0))
-                port = sk.getsockname()[1]
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
         if gloo:
             dist.init_process_group("gloo")
         else:
@@ -219,11 +321,11 @@ def main():
     # this rank's share (pathtrace.dist.RankFrame, also driven by tests/test_dist_gpu.py)
     share = ptdist.RankFrame(ds, W, H, spp, cfg.depth, rank=rank, world=world, split=args.split,
                              screen=cfg.screen, subset=keep, order=args.order, device=local,
-                             max_buffer_bytes=40 << 30, force_split=use_dist)
+                             max_buffer_bytes=40 << 30, force_split=use_dist, tile=args.tile, deal=args.deal)
     kernel_key = ds.kernel_key(cfg.depth)
     # lane-walk scenes render in split launches (runtime.cpp: pt_render_light over every chunk, then
     # pt_render_fast over the chunks it left; PT_SPLIT=0 turns them off); one render = one "launch" here
-    split = cfg.lane_walk and args.order == "fast" and os.environ.get("PT_SPLIT", "1") != "0"
+    split = cfg.lane_walk and args.order == "fast" and split_launches_env()
     render_kernels = "pt_render_light + pt_render_fast" if split else "pt_render_fast"
     by_samples, mine = share.by_samples, share.pixels
     fb = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
@@ -297,7 +399,8 @@ def main():
                        "sharding": (("one GPU renders every pixel" if not subset else
                                      "one GPU renders %d hashed pixels of the frame" % subset) if not use_dist else
                                     ("every pixel, spp split over ranks, per-pixel sums" if by_samples
-                                     else "16x16 tiles hashed over ranks") +
+                                     else "%dx%d tiles, %s deal over ranks" % (
+                                         share.tile, share.tile, args.deal)) +
                                     (" + gloo reduce through host memory (rehearsal: %d ranks on %d GPU(s))" %
                                      (world, torch.cuda.device_count()) if gloo else " + RCCL reduce")) +
                                    (" (--force-dist: the N > 1 step at world size %d)" % world

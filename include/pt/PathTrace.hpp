@@ -809,6 +809,19 @@ inline uint64_t edgeColumnSeed(uint64_t seed, int x)
     return z ^ (z >> 31);
 }
 
+/* the engine key of pixel (px, py) on a frame W wide (a column past the right
+ * edge is keyed on its own grid, x + 1 wide); throws on a coordinate no key exists for */
+inline int64_t pixelKeyIndex(int px, int py, int W)
+{
+    if (px < 0 || py < 0)
+        throw std::invalid_argument("tracePixel: negative pixel coordinate");
+    const int gw = px < W ? W : px + 1;
+    const int64_t i = (int64_t)py * gw + px;
+    if (i > INT32_MAX)
+        throw std::invalid_argument("tracePixel: pixel index out of range");
+    return i;
+}
+
 inline void tracePixels(SpanIterator &spanIterator, const int32_t *px, const int32_t *py, size_t n, Color *colors,
                         int screenXResolution, int screenYResolution, int sampleCount, int rayDepth, float screenWidth,
                         float screenHeight, float screenDistance, const FrameEngine &engine)
@@ -825,12 +838,7 @@ inline void tracePixels(SpanIterator &spanIterator, const int32_t *px, const int
     std::vector<size_t> in_at;
     std::map<int, std::vector<size_t>> edge; /* column x >= W -> batch positions */
     for (size_t k = 0; k < n; k++) {
-        if (px[k] < 0 || py[k] < 0)
-            throw std::invalid_argument("tracePixel: negative pixel coordinate");
-        const int gw = px[k] < W ? W : px[k] + 1;
-        const int64_t i = (int64_t)py[k] * gw + px[k];
-        if (i > INT32_MAX)
-            throw std::invalid_argument("tracePixel: pixel index out of range");
+        const int64_t i = pixelKeyIndex(px[k], py[k], W);
         if (px[k] < W) {
             in_pix.push_back((int32_t)i);
             in_at.push_back(k);
@@ -1007,6 +1015,7 @@ public:
 
     Color tracePixel(int px, int py)
     {
+        (void)pixelKeyIndex(px, py, W_); /* a bad coordinate fails its own caller, not the batch it would join */
         Req r;
         r.x = px, r.y = py;
         std::unique_lock<std::mutex> lk(m_);

@@ -160,8 +160,24 @@ typedef struct pt_render_stats {
  * for each pixel of params->pixels (or of the whole frame, row-major), the
  * mean radiance (r, g, b) exactly as tracePixel returns it (path-trace.h:187-201).
  * Replaces the per-pixel tracePixel calls of RenderBlock::calcPixelColor
- * (reference src/test.cpp:441-465). */
+ * (reference src/test.cpp:441-465).  stats = NULL skips the launches' timing
+ * events and the counter read-back (the per-pixel caller's fast path). */
 int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_stats *stats);
+
+/* Host-clock phases (microseconds) of the calling thread's last pt_render --
+ * the breakdown of a per-pixel tracePixel call.  out[k]
+ * for k < n: */
+#define PT_PROF_TOTAL 0   /* the whole call                                                   */
+#define PT_PROF_SETUP 1   /* validation, the scene's generated module (cached), device buffers */
+#define PT_PROF_ENQUEUE 2 /* pixel upload, counter reset, render + reduce launches (with
+                             stats: also the wait for their timing events)                   */
+#define PT_PROF_WAIT 3    /* stream synchronise: the kernels' remaining run time              */
+#define PT_PROF_D2H 4     /* the result's copy to host memory                                 */
+#define PT_PROF_KERNEL 5  /* render launch(es) by HIP events (0 unless stats were asked for,
+                             or PT_CALL_KERNEL_TIME is set)                                   */
+#define PT_PROF_REDUCE 6  /* pt_reduce by HIP events (the same condition)                     */
+#define PT_PROF_N 7
+int pt_call_profile(double *out, int n);
 
 /* Device variant: writes W*H*3 floats into device memory fb (full frame,
  * row-major; with params->pixels, 3 floats at 3*index for every listed index,
@@ -174,7 +190,11 @@ int pt_render_device(pt_scene *s, const pt_render_params *p, float *fb, void *st
  * events around each launch and the device counters accumulate on the scene's
  * device until pt_render_collect, so a caller can queue the render, a
  * collective on the same stream and more renders without a host round trip
- * (bench.py's multi-GPU step: render, then the RCCL reduce of the frame). */
+ * (bench.py's multi-GPU step: render, then the RCCL reduce of the frame).
+ * At most 1024 timed renders may wait for a collect (PT_ERR_ARG after that).
+ * An untimed pt_render_device queued while timed renders wait joins them: its
+ * launches are timed and its counters go into the next collect's totals, and
+ * it never counts against the cap. */
 int pt_render_device_timed(pt_scene *s, const pt_render_params *p, float *fb, void *stream);
 
 /* Waits for the timed renders queued on `device` since the last collect and
@@ -209,6 +229,10 @@ int pt_render_adaptive(pt_scene *s, const pt_render_params *p, pt_adaptive_param
  * strength) of include/path-trace.h:58-165 for a batch of caller rays, in one
  * device launch.  rays = n records of 7 floats: origin xyz, direction xyz
  * (non-zero: Ray's assert, include/ray.h:17; not normalised), strength.
+ * Origin and direction components must be finite (PT_ERR_ARG otherwise): the
+ * kernel's axis-aligned plane forms keep only the product that is non-zero for
+ * finite operands, where the reference's full dot product of an infinite
+ * component would be NaN.
  * rgb_out receives, per ray, the mean of spp traceRay samples -- sample s of ray
  * k drawing from the engine keyed (seed, ray_begin + k, sample_begin + s), include/pt/
  * pt_engine.h -- summed in `order` and divided by spp: with spp = 1 the

@@ -58,6 +58,7 @@ struct ObjRec
 };
 
 struct DeviceState; /* runtime.cpp */
+struct Generated;
 
 struct SceneImpl
 {
@@ -75,9 +76,13 @@ struct SceneImpl
     std::map<int, std::unique_ptr<DeviceState>> devices;
     std::shared_ptr<struct QueryCache> qcache; /* loaded query modules (runtime.cpp) */
     std::string last_key;
+    /* generated render modules by a fingerprint of everything generate() reads
+     * (runtime.cpp generated(): per-call callers skip the ~200 KB source text) */
+    std::map<uint64_t, std::shared_ptr<const Generated>> gen_cache;
     void clear()
     {
         images.clear(), textures.clear(), materials.clear(), objects.clear();
+        gen_cache.clear();
         qcache.reset(); /* its modules hold copies of the old images */
         root = -1;
         default_tex[0] = default_tex[1] = -1;

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -45,6 +46,16 @@ namespace pt
 
 thread_local std::string g_error;
 void set_error(const std::string &msg) { g_error = msg; }
+
+/* Host-clock phases of this thread's last pt_render (pt_call_profile). */
+thread_local double g_prof[PT_PROF_N];
+double now_us()
+{
+    return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+               .count() /
+           1e3;
+}
 
 #define HIPCHECK(x)                                                                                  \
     do {                                                                                             \
@@ -129,6 +140,7 @@ struct DeviceState
     std::vector<int> img_ids;
     DevBuf<uint64_t> jump;
     DevBuf<float> stage, accum, fb;
+    DevBuf<float> out; /* pt_render's output (grow-only: no allocation per call) */
     DevBuf<int> pixels;
     DevBuf<uint64_t> stats;
     std::vector<PendingRender> pending; /* deferred timings (pt_render_device_timed) */
@@ -139,6 +151,7 @@ struct DeviceState
             for (auto &pr : pending)
                 for (auto e : pr.evs) (void)hipEventDestroy(e);
             P.release(), imgs.release(), jump.release(), stage.release(), accum.release(), fb.release();
+            out.release();
             pixels.release(), stats.release();
             for (auto &b : img_data) b.release();
             if (mod)
@@ -656,11 +669,76 @@ size_t stage_floats(const pt_render_params *p, long long npix, long long per_pas
     return std::min(n, (size_t)(npix * per_pass * 3));
 }
 
+/* generate() is a pure function of the scene records, the depth, the module
+ * kind and the experiment hooks it reads; its text (the ~200 KB device library
+ * plus the scene's types) and the FNV key over it cost about 0.1 ms, which a
+ * caller tracing pixel by pixel (src/test.cpp:450) would pay per call.  A
+ * scene keeps what it generated under a fingerprint of those inputs. */
+struct Fnv
+{
+    uint64_t h = 0xcbf29ce484222325ull;
+    void bytes(const void *p, size_t n)
+    {
+        const unsigned char *b = (const unsigned char *)p;
+        for (size_t k = 0; k < n; k++) h = (h ^ b[k]) * 0x100000001b3ull;
+    }
+    template <class T>
+    void add(const T &v)
+    {
+        bytes(&v, sizeof v);
+    }
+    void str(const char *v)
+    {
+        const size_t n = v ? strlen(v) : (size_t)-1;
+        add(n);
+        if (v)
+            bytes(v, n);
+    }
+};
+std::shared_ptr<const Generated> generated(SceneImpl &s, int depth, bool rays)
+{
+    if (const char *hdr = getenv("PT_DEVICE_HEADER")) /* experiment hook: the file may change under us */
+        if (*hdr)
+            return std::make_shared<const Generated>(generate(s, depth, rays));
+    Fnv f;
+    for (const ObjRec &o : s.objects) {
+        f.add(o.kind), f.add(o.mat), f.add(o.a), f.add(o.b);
+        f.bytes(o.f, sizeof o.f);
+    }
+    f.add(s.objects.size());
+    for (const MatRec &m : s.materials) {
+        f.add(m.reflect), f.add(m.scatter), f.add(m.emissive), f.add(m.transmit), f.add(m.trc), f.add(m.ior);
+    }
+    f.add(s.materials.size());
+    for (const TexRec &t : s.textures) {
+        f.add(t.kind), f.add(t.child);
+        f.bytes(t.f, sizeof t.f), f.bytes(t.img, sizeof t.img);
+    }
+    f.add(s.textures.size());
+    for (const ImageRec &im : s.images) /* images are immutable once created */
+        f.add(im.w), f.add(im.h);
+    f.add(s.images.size());
+    f.add(s.root), f.add(s.default_tex[0]), f.add(s.default_tex[1]);
+    f.add(s.wg_per_cu), f.add(s.fast_spine), f.add(s.lane_walk), f.add(s.lane_scatter);
+    f.add(depth), f.add(rays);
+    f.str(getenv("PT_DEVICE_DEFINES")), f.str(getenv("PT_JIT_OPTIONS"));
+    auto it = s.gen_cache.find(f.h);
+    if (it != s.gen_cache.end())
+        return it->second;
+    if (s.gen_cache.size() >= 16)
+        s.gen_cache.clear();
+    auto g = std::make_shared<const Generated>(generate(s, depth, rays));
+    s.gen_cache[f.h] = g;
+    return g;
+}
+
 /* Module, parameters and every device buffer a render with p needs. */
-DeviceState &prepare(SceneImpl &s, const pt_render_params *p, Generated &g, bool rays = false)
+DeviceState &prepare(SceneImpl &s, const pt_render_params *p, std::shared_ptr<const Generated> &gp,
+                     bool rays = false)
 {
     validate(p);
-    g = generate(s, p->depth, rays);
+    gp = generated(s, p->depth, rays);
+    const Generated &g = *gp;
     s.last_key = g.key;
     DeviceState &ds = device_state(s, p->device, g, rays);
     const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
@@ -752,15 +830,19 @@ constexpr size_t kMaxPending = 1024; /* deferred renders a device keeps before a
 void render_device(SceneImpl &s, const pt_render_params *p, float *fb, hipStream_t stream, pt_render_stats *st,
                    Timing tm, bool compact = false, const float *rays = nullptr, int64_t ray0 = 0)
 {
-    Generated g;
-    DeviceState &ds = prepare(s, p, g, rays != nullptr);
+    std::shared_ptr<const Generated> gp;
+    DeviceState &ds = prepare(s, p, gp, rays != nullptr);
+    const Generated &g = *gp;
     const long long npix = p->pixels ? (long long)p->npixels : (long long)p->width * p->height;
     /* an untimed render queued while timed ones wait for their collect joins
      * them: its launches are timed too, so the counters the collect reads and
-     * the kernel times it sums cover the same renders */
-    if (tm == Timing::None && !ds.pending.empty())
+     * the kernel times it sums cover the same renders.  The pending cap binds
+     * only renders the caller asked to time: a plain render never fails
+     * because of another call's uncollected timings */
+    const bool joined = tm == Timing::None && !ds.pending.empty();
+    if (joined)
         tm = Timing::Deferred;
-    if (tm == Timing::Deferred && ds.pending.size() >= kMaxPending)
+    if (tm == Timing::Deferred && !joined && ds.pending.size() >= kMaxPending)
         throw Error(PT_ERR_ARG, "too many timed renders pending: call pt_render_collect");
     if (tm == Timing::Sync) {
         memset(st, 0, sizeof(*st));
@@ -1390,7 +1472,7 @@ const char *pt_scene_kernel_key(pt_scene *s, int depth)
 int pt_prepare(pt_scene *s, const pt_render_params *p)
 {
     return guard([&] {
-        Generated g;
+        std::shared_ptr<const Generated> g;
         prepare(S(s), p, g);
         return PT_OK;
     });
@@ -1435,30 +1517,52 @@ int pt_render_collect(pt_scene *s, int device, pt_render_stats *stats)
 
 int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_stats *stats)
 {
+    const double t0 = now_us();
+    for (double &v : g_prof) v = 0.0;
     return guard([&] {
         if (!rgb_out)
             throw Error(PT_ERR_ARG, "null output");
         validate(p);
         SceneImpl &sc = S(s);
         HIPCHECK(hipSetDevice(p->device));
-        /* a pixel list renders into a compact buffer, pixel k at 3k */
+        /* a pixel list renders into a compact buffer, pixel k at 3k; pt_reduce
+         * writes every slot of it, so the buffer needs no clearing */
         const size_t n = p->pixels ? (size_t)std::max<int64_t>(1, p->npixels) * 3 : frame_floats(p);
-        DevBuf<float> fb;
-        fb.ensure(n);
-        struct Free
-        {
-            DevBuf<float> &b;
-            ~Free() { b.release(); }
-        } fr{fb};
-        HIPCHECK(hipMemset(fb.p, 0, n * 4));
+        std::shared_ptr<const Generated> gp;
+        DeviceState &ds = prepare(sc, p, gp, false);
+        ds.out.ensure(n);
+        const double t1 = now_us();
+        /* without stats the launches carry no events and no counter read-back */
         pt_render_stats local;
-        render_device(sc, p, fb.p, nullptr, stats ? stats : &local, Timing::Sync, true);
-        HIPCHECK(hipDeviceSynchronize());
+        const bool want = stats != nullptr || getenv("PT_CALL_KERNEL_TIME");
+        render_device(sc, p, ds.out.p, nullptr, stats ? stats : &local, want ? Timing::Sync : Timing::None, true);
+        const double t2 = now_us();
+        HIPCHECK(hipStreamSynchronize(nullptr));
+        const double t3 = now_us();
         const size_t nout = p->pixels ? (size_t)p->npixels * 3 : n;
         if (nout)
-            HIPCHECK(hipMemcpy(rgb_out, fb.p, nout * 4, hipMemcpyDeviceToHost));
+            HIPCHECK(hipMemcpy(rgb_out, ds.out.p, nout * 4, hipMemcpyDeviceToHost));
+        const double t4 = now_us();
+        g_prof[PT_PROF_SETUP] = t1 - t0;
+        g_prof[PT_PROF_ENQUEUE] = t2 - t1;
+        g_prof[PT_PROF_WAIT] = t3 - t2;
+        g_prof[PT_PROF_D2H] = t4 - t3;
+        g_prof[PT_PROF_TOTAL] = t4 - t0;
+        if (want) {
+            const pt_render_stats &st = stats ? *stats : local;
+            g_prof[PT_PROF_KERNEL] = st.kernel_ms * 1e3;
+            g_prof[PT_PROF_REDUCE] = st.reduce_ms * 1e3;
+        }
         return PT_OK;
     });
+}
+
+int pt_call_profile(double *out, int n)
+{
+    if (!out || n < 0)
+        return PT_ERR_ARG;
+    for (int k = 0; k < n && k < PT_PROF_N; k++) out[k] = g_prof[k];
+    return PT_OK;
 }
 
 /* traceRay<T>(ray, spanIterator, depth, engine, strength), include/path-trace.h:
@@ -1499,9 +1603,19 @@ int pt_trace_rays(pt_scene *s, const pt_trace_params *tp, const float *rays, int
         }
         if (!rays || !rgb_out)
             throw Error(PT_ERR_ARG, "null rays or output");
-        for (int64_t k = 0; k < n; k++) /* Ray(o, d) asserts d != 0 (include/ray.h:17) */
+        for (int64_t k = 0; k < n; k++) {
+            /* Ray(o, d) asserts d != 0 (include/ray.h:17) */
             if (rays[7 * k + 3] == 0.0f && rays[7 * k + 4] == 0.0f && rays[7 * k + 5] == 0.0f)
                 throw Error(PT_ERR_ARG, "ray " + std::to_string(k) + " has a zero direction");
+            /* The kernel's axis-aligned plane forms take d.n as the one product
+             * that survives for finite operands (the other terms are +-0); an
+             * infinite or NaN component would make the reference's full dot
+             * product NaN where the device has a number, so such rays are
+             * refused rather than traced differently. */
+            for (int c = 0; c < 6; c++)
+                if (!std::isfinite(rays[7 * k + c]))
+                    throw Error(PT_ERR_ARG, "ray " + std::to_string(k) + " has a non-finite origin or direction");
+        }
         SceneImpl &sc = S(s);
         HIPCHECK(hipSetDevice(p.device));
         DevBuf<float> fb, rb;

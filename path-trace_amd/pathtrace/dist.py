@@ -1,19 +1,32 @@
 """Multi-GPU sharding of one frame.
 
-The frame is cut into 16x16 tiles dealt round-robin to ranks in hashed order
-(interleaved: tile cost varies by ~10^3 between sky and diffuse regions, so
-contiguous bands would load-imbalance).  Every pixel has exactly one owner
-and its samples are seeded by its global index, so each rank writes its own
-pixels into a zero-initialised full-frame float3 buffer and one sum-reduce
-over RCCL/xGMI (or gloo on CPU) assembles a frame that is bit-identical to a
+The frame is cut into square tiles and every tile has exactly one owner.  Each
+pixel's samples are seeded by its global index, so each rank writes its own
+pixels into a zero-initialised full-frame float3 buffer and one sum-reduce over
+RCCL/xGMI (or gloo on CPU) assembles a frame that is bit-identical to a
 single-GPU render (x + 0.0 == x).  This replaces the reference's TCP block farm
 (src/test.cpp:520-778), whose text protocol also moved each pixel exactly once.
+
+Two deals of the tile grid:
+
+* "lattice" (default, 4x4 tiles): tile (tx, ty) -> rank (tx + LATTICE_STEP * ty)
+  mod N.  Any N consecutive tiles of a tile row belong to N different ranks, so
+  every rank holds the same share of every region wider than N tiles.  Tile
+  cost varies by ~10^3 between sky and diffuse regions but is smooth in space,
+  so this stratified deal balances the ranks' work to the cost of a tile edge
+  (tools/shard_times.py, profiles/round6/).
+* "hashed" (the round-2..5 partition, 16x16 tiles): tiles dealt round-robin in
+  a splitmix64-hashed order -- interleaved, but the count of expensive tiles a
+  rank receives is binomial: 1.19 max/mean on C4 at 8 ranks
+  (profiles/round4/shards_c4_8ranks_tiles.jsonl).
 """
 from __future__ import annotations
 
 import numpy as np
 
-TILE = 16
+TILE = 4            # default tile edge (pixels) of the lattice deal
+HASHED_TILE = 16    # the hashed deal's tile edge (rounds 2-5)
+LATTICE_STEP = 3    # rank offset between tile rows: odd, so rows shift by a unit coprime to 2^k
 
 
 def tile_owner(tile_index: np.ndarray, world: int) -> np.ndarray:
@@ -26,17 +39,31 @@ def tile_owner(tile_index: np.ndarray, world: int) -> np.ndarray:
     return (z % np.uint64(world)).astype(np.int64)
 
 
-def rank_pixels(width: int, height: int, rank: int, world: int, tile: int = TILE) -> np.ndarray:
-    """Global pixel indices (y * width + x) owned by `rank`, tile by tile."""
-    if world == 1:
-        return np.arange(width * height, dtype=np.int32)
+def tile_owners(width: int, height: int, world: int, tile: int, deal: str) -> np.ndarray:
+    """owner rank of every tile, shape (tiles_y, tiles_x)"""
     tx = (width + tile - 1) // tile
     ty = (height + tile - 1) // tile
+    if deal == "lattice":
+        xs = np.arange(tx, dtype=np.int64)[None, :]
+        ys = np.arange(ty, dtype=np.int64)[:, None]
+        return (xs + LATTICE_STEP * ys) % world
+    if deal != "hashed":
+        raise ValueError("deal must be 'lattice' or 'hashed'")
     # deal tiles round-robin in hashed order: spatially scattered, counts equal to +-1
     order = np.argsort(tile_owner(np.arange(tx * ty), 1 << 30), kind="stable")
     owners = np.empty(tx * ty, dtype=np.int64)
     owners[order] = np.arange(tx * ty) % world
-    owners = owners.reshape(ty, tx)
+    return owners.reshape(ty, tx)
+
+
+def rank_pixels(width: int, height: int, rank: int, world: int, tile: int = 0, deal: str = "lattice") -> np.ndarray:
+    """Global pixel indices (y * width + x) owned by `rank`, in raster order.
+    tile 0 = the deal's default edge (lattice 4, hashed 16)."""
+    if world == 1:
+        return np.arange(width * height, dtype=np.int32)
+    if tile <= 0:
+        tile = TILE if deal == "lattice" else HASHED_TILE
+    owners = tile_owners(width, height, world, tile, deal)
     ys, xs = np.mgrid[0:height, 0:width]
     mine = owners[ys // tile, xs // tile] == rank
     return (ys * width + xs)[mine].astype(np.int32)
@@ -56,20 +83,23 @@ class RankFrame:
     split "samples": the rank renders every pixel (or `subset`) for samples
     [r*spp/N, (r+1)*spp/N) and writes per-pixel sums (sample_begin / sum_only);
     after the sum-reduce rank 0 divides by spp -- tracePixel's mean with the
-    ranks' partial sums added in rank order.  split "tiles": the rank renders
-    the hashed 16x16 tiles it owns (means); the disjoint frames sum-reduce to
-    the single-GPU frame bit for bit.  One rank is the plain full render."""
+    ranks' partial sums added in rank order.  split "tiles" (the default since
+    round 6): the rank renders the tiles it owns (rank_pixels: `deal`, `tile`)
+    as means; the disjoint frames sum-reduce to the single-GPU frame bit for
+    bit.  One rank is the plain full render."""
 
-    def __init__(self, ds, width, height, spp, depth, rank=0, world=1, split="samples", screen=None,
-                 subset=None, order="fast", device=0, max_buffer_bytes=0, seed=0x5EED, force_split=False):
+    def __init__(self, ds, width, height, spp, depth, rank=0, world=1, split="tiles", screen=None,
+                 subset=None, order="fast", device=0, max_buffer_bytes=0, seed=0x5EED, force_split=False,
+                 tile=0, deal="lattice"):
         from . import make_params
         if split not in ("samples", "tiles"):
             raise ValueError("split must be 'samples' or 'tiles'")
         self.ds, self.rank, self.world, self.spp, self.device = ds, rank, world, spp, device
+        self.tile = tile if tile > 0 else (TILE if deal == "lattice" else HASHED_TILE)
         # force_split: take the N > 1 path even for one rank (per-pixel sums +
         # the reduce + rank 0's division), e.g. bench.py --force-dist
         self.by_samples = (world > 1 or force_split) and split == "samples"
-        mine = rank_pixels(width, height, rank, 1 if self.by_samples else world)
+        mine = rank_pixels(width, height, rank, 1 if self.by_samples else world, tile=tile, deal=deal)
         if subset is not None:
             mine = np.intersect1d(mine, np.asarray(subset)).astype(np.int32)
         self.pixels = mine

@@ -83,6 +83,18 @@ int main(int argc, char **argv)
             }
             if (!ok)
                 return 4;
+            { /* PixelBatcher: a bad coordinate fails its own caller before it joins a batch (no device work) */
+                std::unique_ptr<SpanIterator> it(world->makeSpanIterator());
+                PixelBatcher q(*it, 16, 16, 1, 4, 16, 16, 32);
+                ok = false;
+                try {
+                    q.tracePixel(-1, 3);
+                } catch (std::invalid_argument &) {
+                    ok = true;
+                }
+                if (!ok || q.launches() != 0)
+                    return 5;
+            }
             Matrix r = Matrix::rotateY(0.5);
             Matrix id = r.concat(invert(r));
             printf("errors ok %.6f %.6f\n", id.x00, id.x11);
@@ -289,6 +301,25 @@ int main(int argc, char **argv)
             for (int k = 0; k < ncall; k++)
                 tracePixel(*it, k % W, k / W, W, H, spp, depth, sw, sh, dist, eng);
             const double per_call = secs(t0) / ncall;
+            /* per-call breakdown (pt_call_profile), mean over the calls: the top
+             * rows above (sky: one query per sample) and pixels spread over the
+             * frame (Weyl sequence), plain and with the launches' HIP events */
+            double prof[2][2][PT_PROF_N] = {};
+            for (int timed = 0; timed < 2; timed++) {
+                if (timed)
+                    setenv("PT_CALL_KERNEL_TIME", "1", 1);
+                for (int spread = 0; spread < 2; spread++)
+                    for (int k = 0; k < ncall; k++) {
+                        const long long i = spread ? (long long)((k * 0.6180339887 - (long long)(k * 0.6180339887)) *
+                                                                 (double)(W * H))
+                                                   : k;
+                        tracePixel(*it, (int)(i % W), (int)(i / W), W, H, spp, depth, sw, sh, dist, eng);
+                        double one[PT_PROF_N];
+                        pt_call_profile(one, PT_PROF_N);
+                        for (int j = 0; j < PT_PROF_N; j++) prof[timed][spread][j] += one[j] / ncall;
+                    }
+                unsetenv("PT_CALL_KERNEL_TIME");
+            }
             std::vector<int32_t> xs, ys;
             for (int y = 0; y < H; y++)
                 for (int x = 0; x < W; x++) xs.push_back(x), ys.push_back(y);
@@ -316,8 +347,26 @@ int main(int argc, char **argv)
             FILE *f = fopen(argv[7], "w");
             if (!f)
                 return 5;
+            static const char *names[PT_PROF_N] = {"total", "setup", "enqueue", "wait", "d2h", "kernel", "reduce"};
+            std::string bd = "{";
+            for (int timed = 0; timed < 2; timed++)
+                for (int spread = 0; spread < 2; spread++) {
+                    char b[96];
+                    snprintf(b, sizeof b, "%s\"%s_%s\": {", bd.size() > 1 ? ", " : "", timed ? "events" : "plain",
+                             spread ? "spread_pixels" : "top_rows");
+                    bd += b;
+                    for (int j = 0; j < PT_PROF_N; j++) {
+                        if (!timed && j >= PT_PROF_KERNEL)
+                            continue;
+                        snprintf(b, sizeof b, "%s\"%s\": %.1f", j ? ", " : "", names[j], prof[timed][spread][j]);
+                        bd += b;
+                    }
+                    bd += "}";
+                }
+            bd += "}";
+            fprintf(f, "{\"per_call_breakdown_us\": %s, ", bd.c_str());
             fprintf(f,
-                    "{\"W\": %d, \"H\": %d, \"spp\": %d, \"depth\": %d, \"threads\": %d, "
+                    "\"W\": %d, \"H\": %d, \"spp\": %d, \"depth\": %d, \"threads\": %d, "
                     "\"per_call_us\": %.1f, \"per_call_calls\": %d, \"batch_s\": %.6f, \"batch_us_per_pixel\": %.3f, "
                     "\"batcher_s\": %.6f, \"batcher_launches\": %llu, \"batcher_mean_batch\": %.1f, "
                     "\"batcher_us_per_pixel\": %.3f}\n",

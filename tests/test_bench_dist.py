@@ -24,10 +24,10 @@ def _free_port():
     return port
 
 
-def _bench(args, nproc, tmp_path, name, env_extra=None):
+def _bench(args, nproc, tmp_path, name, env_extra=None, torchrun=True):
     frame = str(tmp_path / (name + ".npy"))
     cmd = [sys.executable, "-u"]
-    if nproc > 1:
+    if nproc > 1 and torchrun:
         cmd += ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port())]
     cmd += [os.path.join(ROOT, "bench.py"), "--gpus", str(nproc)] + args + ["--dump-frame", frame]
@@ -85,3 +85,30 @@ def test_bench_force_dist_rccl_world1(tmp_path):
     assert d["queries_per_sample"] == pytest.approx(one["queries_per_sample"], rel=1e-9)
     assert d["roofline"]["traffic"] is None and "default one-GPU command" in d["roofline"]["traffic_note"]
     np.testing.assert_array_equal(f2.view(np.uint32), f1.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_bench_gpus_two_without_torchrun(tmp_path):
+    """`bench.py --gpus 2` with no torchrun starts the two ranks
+    itself (here over gloo, both on the box's one GPU) and reports n_gpus 2;
+    the default partition (4x4 tiles, lattice deal) reduces to the one-rank
+    frame bit for bit."""
+    common = ["--config", "C3", "--spp", "64", "--steps", "1", "--warmup", "0", "--no-cpu"]
+    one, f1 = _bench(common, 1, tmp_path, "one")
+    two, f2 = _bench(common + ["--backend", "gloo"], 2, tmp_path, "two", torchrun=False)
+    assert two["n_gpus"] == 2
+    assert "4x4 tiles, lattice deal" in two["config"]["sharding"]
+    assert two["samples_per_step"] == one["samples_per_step"]
+    np.testing.assert_array_equal(f2.view(np.uint32), f1.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_bench_more_gpus_than_the_box_has(tmp_path):
+    """--gpus 3 over RCCL on a one-GPU box exits non-zero without a line"""
+    import torch
+    n = torch.cuda.device_count() + 2
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--no-cpu"],
+                       capture_output=True, text=True, timeout=120, cwd=ROOT,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert r.returncode != 0 and "GPU(s) visible" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -158,3 +158,9 @@ def test_facade_pixel_batcher(facade_bin, tmp_path):
     d = json.load(open(out))
     assert d["per_call_us"] > 0 and d["batcher_launches"] >= 1
     assert d["batcher_launches"] < 48 * 32 / 2
+    bd = d["per_call_breakdown_us"]  # pt_call_profile: the phases of one call add up to it
+    for k, ph in bd.items():
+        parts = ph["setup"] + ph["enqueue"] + ph["wait"] + ph["d2h"]
+        assert 0 < parts <= ph["total"] * 1.001 + 1, (k, ph)
+        if k.startswith("events"):
+            assert ph["kernel"] > 0 and ph["reduce"] > 0, (k, ph)

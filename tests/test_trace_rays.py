@@ -50,6 +50,17 @@ def test_trace_rays_rejects_zero_direction(built):
         pt.trace_rays(ds, r, depth=4)
 
 
+@pytest.mark.parametrize("col,val", [(3, np.inf), (5, -np.inf), (4, np.nan), (0, np.inf), (2, np.nan)])
+def test_trace_rays_rejects_non_finite(built, col, val):
+    """the axis-aligned plane forms assume finite operands, so a
+    non-finite origin or direction is refused before any device work"""
+    ds = pt.DeviceScene(T.build("scene_p1"))
+    r = T.trace_rays_input(4, seed=3)
+    r[1, col] = val
+    with pytest.raises(pt.PtError, match="non-finite"):
+        pt.trace_rays(ds, r, depth=4)
+
+
 def test_trace_rays_empty_batch(built):
     out = pt.trace_rays(pt.DeviceScene(T.build("scene_p1")), np.zeros((0, 7), np.float32), depth=4)
     assert out.shape == (0, 3)

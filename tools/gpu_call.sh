@@ -16,15 +16,16 @@
 #   benchab:CFG:REPS:S1|S2   whole bench.py runs (--no-cpu) under env specs, interleaved
 #                         (tools/ab/bench_env.sh; spec "-" or VAR=value[,VAR=value])
 #   phase:SPP             PT_PHASE_TIMING phase split of the C3 frame (tools/phase_probe.py)
+#   shards:CFG:WORLD:SPP:SPLIT:TILE:DEAL   tools/shard_times.py (each rank's share on this GPU)
 #   evidence:CFG          the bench line's evidence, bound to the timed code object:
-#                         PMC passes (tools/pmc_bench.sh) -> profiles/round5/pmc_bench_CFG.json,
+#                         PMC passes (tools/pmc_bench.sh) -> profiles/round6/pmc_bench_CFG.json,
 #                         then bench.py under rocprofv3 --kernel-trace --stats ->
-#                         profiles/round5/bench_CFG_{rocprof.json,kernel_stats.csv}
-#                         (also kept under OUTDIR/round5/: only gpurun_out/ comes back from the box)
+#                         profiles/round6/bench_CFG_{rocprof.json,kernel_stats.csv}
+#                         (also kept under OUTDIR/round6/: only gpurun_out/ comes back from the box)
 OUT=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$OUT"; OUT=$(cd "$OUT" && pwd)
-PROF="$ROOT/profiles/round5"; mkdir -p "$PROF"
+PROF="$ROOT/profiles/round6"; mkdir -p "$PROF"
 cd "$ROOT"
 run() {  # run LIMIT LOG cmd...
     lim=$1; log=$2; shift 2
@@ -66,6 +67,11 @@ for step in "$@"; do
   benchab)
     IFS='|' read -r -a SP <<< "$c"
     run 1500 "$OUT/benchab_$a.txt" bash tools/ab/bench_env.sh "$a" "$b" "${SP[@]}"; cat "$OUT/benchab_$a.txt" ;;
+  shards)
+    IFS=: read -r _ a b c d e f <<< "$step"
+    tag="${a}_${b}_${c}_${d}_${e}_${f}"
+    run 900 "$OUT/shards_$tag.jsonl" python3 tools/shard_times.py "$a" "$b" "$c" "$d" "$e" "$f"
+    tail -1 "$OUT/shards_$tag.jsonl" ;;
   phase)
     run 600 "$OUT/phase_$a.txt" python3 tools/phase_probe.py "$a"; cat "$OUT/phase_$a.txt" ;;
   evidence)
@@ -76,7 +82,7 @@ for step in "$@"; do
     rc=$?; [ $rc -eq 0 ] || { echo "FAILED rc=$rc: rocprofv3 bench $a"; tail -20 "$OUT/prof_$a.log"; exit $rc; }
     grep '^{' "$OUT/prof_$a.log" > "$PROF/bench_${a}_rocprof.json"
     cp "$(find "$OUT/prof_$a" -name '*kernel_stats.csv' | head -1)" "$PROF/bench_${a}_kernel_stats.csv"
-    mkdir -p "$OUT/round5"; cp "$PROF/pmc_bench_$a.json" "$PROF/bench_${a}_rocprof.json" "$PROF/bench_${a}_kernel_stats.csv" "$OUT/round5/"
+    mkdir -p "$OUT/round6"; cp "$PROF/pmc_bench_$a.json" "$PROF/bench_${a}_rocprof.json" "$PROF/bench_${a}_kernel_stats.csv" "$OUT/round6/"
     cut -c1-300 "$PROF/bench_${a}_rocprof.json"; head -3 "$PROF/bench_${a}_kernel_stats.csv" ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
