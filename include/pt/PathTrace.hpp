@@ -364,7 +364,8 @@ public:
     /* getColor / getFloat (texture.h:13-18).  The built-in classes answer on
      * the device (pt_tex_eval of this texture, flattened once); a user-defined
      * subclass overrides getColor as in the reference -- it then works on the
-     * host, but has no device form, so a scene using it cannot be rendered.
+     * host -- and gets a device form (renders, device lookups) by giving its
+     * body as device source (deviceGetColor below).
      * The built-in classes are final and their fields const (Image is
      * immutable too), so the flattened form cached on first use never goes
      * stale and no override can be bypassed by the device path. */
@@ -377,7 +378,7 @@ public:
     }
     virtual float getFloat(Vector3D pos) const
     {
-        if (!device_form_) { /* the reference's default: the mean of getColor */
+        if (!device_form_ && !deviceGetFloat()) { /* the reference's default: the mean of getColor */
             Color c = getColor(pos);
             return (c.x + c.y + c.z) * (1.0f / 3.0f);
         }
@@ -390,9 +391,22 @@ public:
     void getColors(const Vector3D *pos, size_t n, Color *colors, float *values) const { eval(pos, n, colors, values); }
     virtual Texture *duplicate() const = 0;
     virtual Texture *transform(const Matrix &) const { return nullptr; }
-    virtual pt_id flatten(Flattener &) const
+    /* The device form of a user-defined subclass (pt_tex_device): its getColor
+     * -- and getFloat, if it overrides the default -- as device source over
+     * `V3 p` and its parameters `const float *prm` (deviceParams).  Give the
+     * same arithmetic as the host override and the device computes the same
+     * bits (the module is built without FMA contraction). */
+    virtual const char *deviceGetColor() const { return nullptr; }
+    virtual const char *deviceGetFloat() const { return nullptr; }
+    virtual std::vector<float> deviceParams() const { return std::vector<float>(); }
+    virtual pt_id flatten(Flattener &f) const
     {
-        throw DeviceError(PT_ERR_ARG, "a user-defined Texture subclass has no device form");
+        const char *body = deviceGetColor();
+        if (!body)
+            throw DeviceError(PT_ERR_ARG, "a user-defined Texture subclass has no device form "
+                                          "(override deviceGetColor)");
+        const std::vector<float> prm = deviceParams();
+        return ptCheck(pt_tex_device(f.s, body, deviceGetFloat(), prm.data(), (int)prm.size()));
     }
 
 protected:

@@ -78,6 +78,21 @@ pt_id pt_tex_mirrorball(pt_scene *s, pt_id t);                           /* Mirr
 pt_id pt_tex_spherical(pt_scene *s, pt_id t);                            /* SphericalCoordinatesSkymapTexture :61-85 */
 pt_id pt_tex_transformed(pt_scene *s, const float m[12], pt_id t);      /* TransformedTexture texture.h:60-90 */
 pt_id pt_tex_coord(pt_scene *s);                                         /* test instrument: colour = coordinate */
+/* A user-defined Texture subclass (include/texture.h:10-27: the virtual
+ * getColor, and getFloat unless it keeps the default mean of getColor) as
+ * device source.  color_body is the body of
+ *     V3 getColor(V3 p)           -- p.x, p.y, p.z: the lookup point
+ * and value_body (NULL = the reference's default) the body of
+ *     float getFloat(V3 p)
+ * in the device library's vocabulary (V3, mk(x, y, z), the f32 math builtins
+ * floorf, fabsf, sqrtf, fminf, ...); both read their nparams parameters as
+ * `const float *prm`.  The bodies are compiled into every module of the scene
+ * that reaches the texture, with the scene's options: no FMA contraction and
+ * correctly rounded '/' and sqrt, so a body computes what the same text
+ * compiled on the host with -ffp-contract=off computes.  A body that does not
+ * compile makes the render fail with PT_ERR_COMPILE and the compiler's log in
+ * pt_last_error(). */
+pt_id pt_tex_device(pt_scene *s, const char *color_body, const char *value_body, const float *params, int nparams);
 
 /* ---------------------------------------------------------- materials --- */
 /* Material(reflect, scatter_coefficient, emissive, transmit, ior,

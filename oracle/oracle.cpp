@@ -234,6 +234,41 @@ struct CoordTex : Tex
     V3 color(V3 p) const override { return p; }
 };
 
+/* A user-defined Texture subclass (include/texture.h:10-27): the host functions
+ * a test registered for its slot (the same source the product compiles into
+ * the device module through pt_tex_device, built here with -ffp-contract=off) */
+typedef void (*user_color_fn)(const float *p, const float *prm, float *out);
+typedef float (*user_value_fn)(const float *p, const float *prm);
+struct UserFns
+{
+    user_color_fn color = nullptr;
+    user_value_fn value = nullptr;
+};
+std::map<int, UserFns> &user_slots()
+{
+    static std::map<int, UserFns> m;
+    return m;
+}
+struct UserTex : Tex
+{
+    UserFns fn;
+    std::vector<float> prm;
+    V3 color(V3 p) const override
+    {
+        const float q[3] = {p.x, p.y, p.z};
+        float o[3];
+        fn.color(q, prm.data(), o);
+        return V3(o[0], o[1], o[2]);
+    }
+    float value(V3 p) const override
+    {
+        if (!fn.value)
+            return Tex::value(p);
+        const float q[3] = {p.x, p.y, p.z};
+        return fn.value(q, prm.data());
+    }
+};
+
 struct XformTex : Tex /* TransformedTexture, texture.h:60-90 */
 {
     M34 m;
@@ -712,6 +747,16 @@ std::unique_ptr<Tex> make_tex(const scenetext::Desc &d, Scene &s, int id)
         return std::unique_ptr<Tex>(new ConstTex(V3(t.f[0], t.f[1], t.f[2])));
     if (t.type == "coord")
         return std::unique_ptr<Tex>(new CoordTex());
+    if (t.type == "user") {
+        auto it = user_slots().find(t.i[0]);
+        if (it == user_slots().end() || !it->second.color)
+            throw std::runtime_error("oracle: no host function registered for user texture slot " +
+                                     std::to_string(t.i[0]));
+        auto p = new UserTex;
+        p->fn = it->second;
+        p->prm = t.f;
+        return std::unique_ptr<Tex>(p);
+    }
     if (t.type == "image") {
         auto p = new ImageTex;
         p->im = img(0);
@@ -1069,6 +1114,15 @@ using namespace oracle;
 extern "C" {
 
 const char *oracle_last_error() { return g_err.c_str(); }
+
+/* test infrastructure: the host functions of user texture slot `slot` (value may be NULL) */
+int oracle_register_user_texture(int slot, user_color_fn color, user_value_fn value)
+{
+    if (!color)
+        return -1;
+    user_slots()[slot] = UserFns{color, value};
+    return 0;
+}
 
 } // extern "C"
 

@@ -65,6 +65,8 @@ def lib():
         L.oracle_trace_rays.restype = C.c_int
         L.oracle_trace_rays.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int,
                                         C.c_int64, C.c_int, C.c_int, C.c_void_p]
+        L.oracle_register_user_texture.restype = ctypes.c_int
+        L.oracle_register_user_texture.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_kat.restype = ctypes.c_int
         L.oracle_kat.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
         _lib = L
@@ -227,6 +229,15 @@ def ref_render(scene_text: str, W: int, H: int, spp: int, depth: int, screen=Non
     if info:
         return res, json.loads(out.strip().splitlines()[-1])
     return res
+
+
+def register_user_texture(slot: int, color_fn: int, value_fn: int = 0) -> None:
+    """Test infrastructure: the host functions (addresses of
+    void color(const float *p, const float *prm, float *out) and, optionally,
+    float value(const float *p, const float *prm)) the oracle calls for
+    `tex <id> user <slot> ...` records (pathtrace.scene.DeviceTexture)."""
+    if lib().oracle_register_user_texture(int(slot), color_fn, value_fn or None) != 0:
+        raise RuntimeError("oracle_register_user_texture: null color function")
 
 
 def tex_eval(scene_text: str, points: np.ndarray):

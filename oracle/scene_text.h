@@ -21,6 +21,8 @@
  *   tex <id> spherical <tex>               SphericalCoordinatesSkymapTexture :61-85
  *   tex <id> xform <12 f> <tex>            TransformedTexture    include/texture.h:60-90
  *   tex <id> coord                         test-only: getColor(v) = v (pins coordinate maps)
+ *   tex <id> user <slot> <n> <n f>         a user Texture subclass: the host functions registered
+ *                                          for <slot> (oracle_register_user_texture), n parameters
  *   mat <id> <refl> <scat> <emis> <trans> <ior> <trc>   Material include/material.h:10-37
  *   obj <id> sphere <cx> <cy> <cz> <r> <mat>             Sphere   src/sphere.cpp:6-12
  *   obj <id> plane <nx> <ny> <nz> <d> <mat>              Plane    src/plane.cpp:6-9
@@ -136,6 +138,12 @@ inline Desc parse(const std::string &text)
                 it.i = {parse_int(tok[15])};
             } else if (ty == "coord") {
                 need(3);
+            } else if (ty == "user") {
+                if (tok.size() < 5)
+                    throw std::runtime_error("scene_text: wrong operand count in '" + line + "'");
+                it.i = {parse_int(tok[3]), parse_int(tok[4])};
+                need(5 + (size_t)it.i[1]);
+                for (size_t k = 5; k < tok.size(); k++) it.f.push_back(parse_float(tok[k]));
             } else
                 throw std::runtime_error("scene_text: unknown texture " + ty);
             d.textures.push_back(it);

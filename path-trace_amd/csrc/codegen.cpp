@@ -36,6 +36,7 @@ struct Gen
     int xf_depth = 0;          /* TransformedObjects above the node being generated */
     int unit_axis[3] = {0, 0, 0}; /* planes with normal +-e_k outside transforms */
     std::vector<std::pair<size_t, int>> unit_planes; /* (position of the ",U" mark in a node string, axis) */
+    std::map<int, int> user_tex; /* User texture id -> offset of its parameters in P */
 
     explicit Gen(const SceneImpl &sc) : s(sc) {}
 
@@ -201,8 +202,42 @@ struct Gen
             t << "TXf<" << off << "," << tex(x.child) << ">";
             break;
         }
+        case TexKind::User:
+            if (!user_tex.count(id)) {
+                int off = (int)P.size();
+                P.insert(P.end(), x.params.begin(), x.params.end());
+                user_tex[id] = off;
+            }
+            t << "UTex_" << id;
+            break;
         }
         return t.str();
+    }
+
+    /* The user textures' types (pt_tex_device): the caller's bodies see the
+     * lookup point `p` and their parameters `prm`; getFloat defaults to the
+     * reference's mean of getColor (texture.h:14-18). */
+    std::string user_defs() const
+    {
+        std::ostringstream d;
+        for (const auto &u : user_tex) {
+            const TexRec &x = s.textures.at(u.first);
+            d << "struct UTex_" << u.first << " {\n"
+              << "  __device__ static __forceinline__ V3 color(V3 p, const Env &e) {\n"
+              << "    const float *prm = e.P + " << u.second << ";\n    (void)prm;\n"
+              << "#line 1 \"pt_tex_device " << u.first << " getColor\"\n"
+              << x.color_body << "\n  }\n"
+              << "  __device__ static __forceinline__ float value(V3 p, const Env &e) {\n";
+            if (x.value_body.empty()) {
+                d << "    return mean3(color(p, e));\n";
+            } else {
+                d << "    const float *prm = e.P + " << u.second << ";\n    (void)prm;\n"
+                  << "#line 1 \"pt_tex_device " << u.first << " getFloat\"\n"
+                  << x.value_body << "\n";
+            }
+            d << "  }\n};\n";
+        }
+        return d.str();
     }
 };
 
@@ -327,6 +362,7 @@ Generated generate(const SceneImpl &s, int depth, bool rays)
         src << device_library_source() << "\n";
     }
     src << "namespace ptgen {\nusing namespace ptd;\n";
+    src << g.user_defs();
     src << "typedef " << root << " RootT;\n";
     src << "struct Scene {\n  typedef RootT Root;\n";
     auto dispatch = [&](const char *name, const char *ret, const char *fn, std::string MatTypes::*field) {
@@ -406,12 +442,14 @@ Generated generate_query(const SceneImpl &s, int obj, int tex)
     const std::string qroot = obj >= 0 ? g.shared_axes(g.obj(obj), axis_share) : std::string();
     if (axis_share)
         src << "#define PT_AXIS_SHARE " << axis_share << "\n";
+    const std::string qtex = tex >= 0 ? g.tex(tex) : std::string();
     src << device_library_source() << "\n";
     src << "namespace ptgen {\nusing namespace ptd;\n";
+    src << g.user_defs();
     if (obj >= 0)
         src << "typedef " << qroot << " QRoot;\n";
     if (tex >= 0)
-        src << "typedef " << g.tex(tex) << " QTex;\n";
+        src << "typedef " << qtex << " QTex;\n";
     src << "} // namespace ptgen\n";
     if (obj >= 0)
         src << "PT_DEFINE_QUERY(ptgen::QRoot)\n";

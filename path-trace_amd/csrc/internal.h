@@ -31,7 +31,7 @@ struct ImageRec
     std::vector<float> rgba; /* row 0 = top */
 };
 
-enum class TexKind { Color, Image, ImageAlpha, Skybox, SkyboxAlpha, Multiply, Log, MirrorBall, Spherical, Xform, Coord };
+enum class TexKind { Color, Image, ImageAlpha, Skybox, SkyboxAlpha, Multiply, Log, MirrorBall, Spherical, Xform, Coord, User };
 
 struct TexRec
 {
@@ -39,6 +39,9 @@ struct TexRec
     float f[12] = {0};
     int child = -1;   /* inner texture */
     int img[6] = {-1, -1, -1, -1, -1, -1};
+    /* User (pt_tex_device): the caller's device bodies and parameters */
+    std::string color_body, value_body;
+    std::vector<float> params;
 };
 
 struct MatRec

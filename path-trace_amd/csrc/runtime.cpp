@@ -713,6 +713,10 @@ std::shared_ptr<const Generated> generated(SceneImpl &s, int depth, bool rays)
     for (const TexRec &t : s.textures) {
         f.add(t.kind), f.add(t.child);
         f.bytes(t.f, sizeof t.f), f.bytes(t.img, sizeof t.img);
+        f.str(t.color_body.c_str()), f.str(t.value_body.c_str());
+        f.add(t.params.size());
+        if (!t.params.empty())
+            f.bytes(t.params.data(), t.params.size() * sizeof(float));
     }
     f.add(s.textures.size());
     for (const ImageRec &im : s.images) /* images are immutable once created */
@@ -1274,6 +1278,25 @@ pt_id pt_tex_coord(pt_scene *s)
     return guard([&] {
         TexRec t;
         t.kind = TexKind::Coord;
+        return add_tex(S(s), t);
+    });
+}
+
+/* A user-defined Texture subclass (include/texture.h:10-27: getColor, and
+ * getFloat's default unless overridden) as device source, compiled into every
+ * module of the scene that reaches it (codegen.cpp UTex_<id>). */
+pt_id pt_tex_device(pt_scene *s, const char *color_body, const char *value_body, const float *params, int nparams)
+{
+    return guard([&] {
+        if (!color_body || !*color_body)
+            throw Error(PT_ERR_ARG, "pt_tex_device: empty getColor body");
+        if (nparams < 0 || nparams > (1 << 16) || (nparams > 0 && !params))
+            throw Error(PT_ERR_ARG, "pt_tex_device: bad parameter block");
+        TexRec t;
+        t.kind = TexKind::User;
+        t.color_body = color_body;
+        t.value_body = value_body ? value_body : "";
+        t.params.assign(params, params + nparams);
         return add_tex(S(s), t);
     });
 }

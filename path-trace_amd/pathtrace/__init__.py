@@ -20,7 +20,7 @@ import numpy as np
 from . import _lib
 from ._lib import PT_ORDER_FAST, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, TraceParams, load_hdr, \
     load_png, write_bmp, write_hdr
-from .scene import (ColorTexture, CoordTexture, Difference, Image, ImageAlphaTexture, ImageSkyboxAlphaTexture,
+from .scene import (ColorTexture, CoordTexture, DeviceTexture, Difference, Image, ImageAlphaTexture, ImageSkyboxAlphaTexture,
                     ImageSkyboxTexture, ImageTexture, Intersection, LogTexture, Material, Matrix,
                     MirrorBallSkymapTexture, MultiplyTexture, Object, Plane, SphericalCoordinatesSkymapTexture,
                     Sphere, Texture, TransformedObject, TransformedTexture, Union, invert, to_text,
@@ -96,6 +96,10 @@ class DeviceScene:
             return c(L.pt_tex_color(h, *[float(v) for v in t.color]))
         if isinstance(t, CoordTexture):
             return c(L.pt_tex_coord(h))
+        if isinstance(t, DeviceTexture):
+            prm = (ctypes.c_float * max(1, len(t.params)))(*t.params)
+            return c(L.pt_tex_device(h, t.color_body.encode(), t.value_body.encode() if t.value_body else None,
+                                     prm, len(t.params)))
         if isinstance(t, ImageSkyboxAlphaTexture):
             return c(L.pt_tex_skybox_alpha(h, *[self._image(f) for f in t.faces]))
         if isinstance(t, ImageSkyboxTexture):

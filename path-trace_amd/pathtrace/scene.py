@@ -184,6 +184,22 @@ class CoordTexture(Texture):
     kind = "coord"
 
 
+class DeviceTexture(Texture):
+    """A user-defined Texture subclass (reference include/texture.h:10-27) given
+    as device source (pt_tex_device): `color_body` is the body of
+    V3 getColor(V3 p), `value_body` (None = the reference's default mean of
+    getColor) the body of float getFloat(V3 p); both read `params` as
+    `const float *prm`.  `oracle_slot` names the host function the CPU oracle
+    calls for it (oracle_py.register_user_texture, test infrastructure)."""
+    kind = "user"
+
+    def __init__(self, color_body: str, params=(), value_body: Optional[str] = None, oracle_slot: int = 0):
+        self.color_body = color_body
+        self.value_body = value_body
+        self.params = [float(v) for v in params]
+        self.oracle_slot = int(oracle_slot)
+
+
 class ImageTexture(Texture):
     kind = "image"
 
@@ -405,6 +421,8 @@ class _Registry:
             args = " ".join(_hex(c) for c in t.color)
         elif isinstance(t, CoordTexture):
             args = ""
+        elif isinstance(t, DeviceTexture):  # the oracle's host function for the slot + the parameters
+            args = "%d %d %s" % (t.oracle_slot, len(t.params), " ".join(_hex(v) for v in t.params))
         elif isinstance(t, ImageSkyboxTexture):
             args = " ".join(str(self.image(f)) for f in t.faces)
         elif isinstance(t, ImageTexture):

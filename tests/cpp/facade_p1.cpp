@@ -48,6 +48,47 @@ static std::vector<float> read_f32(const char *path)
     return v;
 }
 
+/* A user-defined Texture subclass as the reference's API allows (include/
+ * texture.h:10-27): a 3-D checkerboard.  getColor runs the body on the host;
+ * deviceGetColor hands the same text to the device (pt_tex_device). */
+namespace user
+{
+struct V3
+{
+    float x, y, z;
+};
+inline V3 mk(float x, float y, float z)
+{
+    V3 r;
+    r.x = x, r.y = y, r.z = z;
+    return r;
+}
+#define PT_TEXT(...) #__VA_ARGS__
+#define CHECKER_BODY                                                                  \
+    const float s = prm[0];                                                           \
+    const float k = floorf(p.x * s) + floorf(p.y * s) + floorf(p.z * s);              \
+    const float odd = k - 2.0f * floorf(k * 0.5f);                                    \
+    return odd != 0.0f ? mk(prm[1], prm[2], prm[3]) : mk(prm[4], prm[5], prm[6]);
+inline V3 checker(V3 p, const float *prm) { CHECKER_BODY }
+} // namespace user
+
+class CheckerTexture : public Texture
+{
+public:
+    explicit CheckerTexture(const std::vector<float> &prm) : prm_(prm) {}
+    Color getColor(Vector3D pos) const override
+    {
+        const user::V3 c = user::checker(user::mk(pos.x, pos.y, pos.z), prm_.data());
+        return Color(c.x, c.y, c.z);
+    }
+    Texture *duplicate() const override { return new CheckerTexture(prm_); }
+    const char *deviceGetColor() const override { return PT_TEXT(CHECKER_BODY); }
+    std::vector<float> deviceParams() const override { return prm_; }
+
+private:
+    std::vector<float> prm_;
+};
+
 int main(int argc, char **argv)
 {
     if (argc < 2)
@@ -281,6 +322,40 @@ int main(int argc, char **argv)
             if (!f)
                 return 5;
             fwrite(batch.data(), sizeof(Color), n, f);
+            fclose(f);
+            return 0;
+        }
+        if (!strcmp(argv[1], "usertex") && argc == 7) {
+            /* P0's shape with the floor's emission a user CheckerTexture (tests/
+             * test_user_texture.py CHECKER): the frame, and the host override
+             * against the device body at a few points (exit 18 on a mismatch) */
+            const int W = atoi(argv[2]), H = atoi(argv[3]), spp = atoi(argv[4]), depth = atoi(argv[5]);
+            Material mdiff(new ColorTexture(0.8f), new ColorTexture(1));
+            Material mfloor(new ColorTexture(0), new ColorTexture(0),
+                            new CheckerTexture({2.0f, 1.0f, 0.9f, 0.3f, 0.2f, 0.3f, 1.0f}));
+            std::unique_ptr<Object> w(new Union(new Union(new Sphere(Vector3D(-1, 0, -4), .5f, &mdiff),
+                                                          new Sphere(Vector3D(1, 0, -4), .5f, &mirror)),
+                                                new Union(new Sphere(Vector3D(0, .3f, -5), .5f, &mdiff),
+                                                          new Plane(Vector3D(0, 1, 0), .5f, &mfloor))));
+            const Texture *chk = mfloor.emissive;
+            const Vector3D pts[4] = {Vector3D(0.1f, 0.2f, 0.3f), Vector3D(-0.6f, 0.7f, 1.4f),
+                                     Vector3D(2.5f, -3.5f, 0.25f), Vector3D(-7.25f, -0.5f, -3.0f)};
+            Color dev[4];
+            float val[4];
+            chk->getColors(pts, 4, dev, val);
+            for (int k = 0; k < 4; k++) {
+                const Color h = chk->getColor(pts[k]);
+                if (memcmp(&h, &dev[k], sizeof h))
+                    return 18;
+            }
+            Renderer r(w.get());
+            Renderer::Settings st;
+            st.width = W, st.height = H, st.sampleCount = spp, st.rayDepth = depth;
+            std::vector<Color> img = r.render(st);
+            FILE *f = fopen(argv[6], "wb");
+            if (!f)
+                return 5;
+            fwrite(img.data(), sizeof(Color), img.size(), f);
             fclose(f);
             return 0;
         }

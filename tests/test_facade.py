@@ -164,3 +164,20 @@ def test_facade_pixel_batcher(facade_bin, tmp_path):
         assert 0 < parts <= ph["total"] * 1.001 + 1, (k, ph)
         if k.startswith("events"):
             assert ph["kernel"] > 0 and ph["reduce"] > 0, (k, ph)
+
+
+@pytest.mark.gpu
+def test_facade_user_texture_bitexact(facade_bin, tmp_path):
+    """A C++ Texture subclass with a host getColor override and the same body
+    as deviceGetColor: the device lookups equal the host override bit for bit
+    (checked in the binary, exit 18), and the frame equals the Python mirror's
+    render of the same scene (pathtrace.DeviceTexture with the same text)."""
+    from test_user_texture import facade_user_scene
+    W, H, spp, depth = 40, 24, 4, 6
+    out = str(tmp_path / "img.bin")
+    r = subprocess.run([facade_bin, "usertex", str(W), str(H), str(spp), str(depth), out],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.returncode, r.stderr)
+    got = np.fromfile(out, dtype=np.float32).reshape(-1, 3)
+    want = pt.render(facade_user_scene(), W, H, spp, depth).reshape(-1, 3)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
