@@ -46,9 +46,11 @@ sys.path[:0] = [os.path.join(ROOT, "path-trace_amd"), os.path.join(ROOT, "oracle
 
 VALU_PEAK_TOPS = 78.6  # 256 CU x 128 FP32 lanes/clk x 2.4 GHz, no FMA (contraction off for parity)
 # SURVEY.md s8(d) op model calibrated by tools/calibrate_ops.py (oracle event
-# counts on hashed pixels): C3 8192 px x 32 spp, C2 512 px x 4 spp, C5 8192 px x 64 spp
-# (C5's texture work -- spherical/skybox maps -- is outside the op model)
-OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 614.78, "C5": 554.13}
+# counts on hashed pixels): C3 8192 px x 32 spp, C2 512 px x 4 spp, C5 8192 px x 64 spp.
+# Since round 6 it counts the texture maps' work too (one weight per texture
+# evaluation by class, calibrate_ops.TEX_W): C2's mirror-ball sky 37.19 ops per
+# query, C5's spherical sky + skybox 125.65; C3 has constant textures only.
+OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 651.97, "C5": 679.78}
 # Counter evidence of this same command (tools/evidence.sh -> tools/pmc_bench.sh:
 # rocprofv3 --pmc passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 +
 # WRITE_SIZE).  Each file records the code-object key of the kernel its passes

@@ -210,6 +210,11 @@ struct Img
     }
 };
 
+/* Texture evaluations by class on this thread (the op model's texture terms,
+ * tools/calibrate_ops.py; SURVEY.md s8(d) counts only geometry and shading) */
+enum TexCount { TC_XFORM, TC_MULTIPLY, TC_IMAGE, TC_SPHERICAL, TC_MIRRORBALL, TC_SKYBOX, TC_LOG, TC_N };
+thread_local uint64_t tl_tex[TC_N];
+
 struct Tex
 {
     virtual ~Tex() {}
@@ -273,14 +278,15 @@ struct XformTex : Tex /* TransformedTexture, texture.h:60-90 */
 {
     M34 m;
     std::unique_ptr<Tex> t;
-    V3 color(V3 p) const override { return t->color(m.apply(p)); }
-    float value(V3 p) const override { return t->value(m.apply(p)); }
+    V3 color(V3 p) const override { return tl_tex[TC_XFORM]++, t->color(m.apply(p)); }
+    float value(V3 p) const override { return tl_tex[TC_XFORM]++, t->value(m.apply(p)); }
 };
 
 /* nearest-texel lookup of ImageTexture / ImageAlphaTexture (image_texture.h:18-28, :44-65):
  * `x -= floor(x)` calls ::floor(double); the difference is exact in float either way. */
 inline void planar_texel(const Img &im, V3 v, int &xi, int &yi)
 {
+    tl_tex[TC_IMAGE]++;
     float x = v.x, y = v.y;
     x = (float)((double)x - ::floor((double)x));
     y = (float)((double)y - ::floor((double)y));
@@ -365,6 +371,7 @@ struct SkyboxTex : Tex
     bool alpha = false;
     float lookup(V3 v, bool want_alpha, V3 &rgb) const
     {
+        tl_tex[TC_SKYBOX]++;
         float fx, fy;
         int f = skybox_face(v, fx, fy);
         int xi, yi;
@@ -399,7 +406,7 @@ struct MultiplyTex : Tex /* filter_texture.h:36-56 */
 {
     V3 f;
     std::unique_ptr<Tex> t;
-    V3 color(V3 p) const override { return t->color(p) * f; }
+    V3 color(V3 p) const override { return tl_tex[TC_MULTIPLY]++, t->color(p) * f; }
 };
 
 struct LogTex : Tex /* filter_texture.h:58-82 */
@@ -413,6 +420,7 @@ struct LogTex : Tex /* filter_texture.h:58-82 */
     }
     V3 color(V3 p) const override
     {
+        tl_tex[TC_LOG]++;
         V3 c = t->color(p);
         return V3(lg(c.x), lg(c.y), lg(c.z));
     }
@@ -423,6 +431,7 @@ struct MirrorBallTex : Tex /* transform_texture.h:33-59 */
     std::unique_ptr<Tex> t;
     static V3 map(V3 v)
     {
+        tl_tex[TC_MIRRORBALL]++;
         if (v == V3(0))
             return V3(0);
         v = normalize(v);
@@ -447,6 +456,7 @@ struct SphericalTex : Tex
     std::unique_ptr<Tex> t;
     static V3 map(V3 v)
     {
+        tl_tex[TC_SPHERICAL]++;
         if (v == V3(0))
             return V3(0);
         v = normalize(v);
@@ -499,8 +509,10 @@ struct Stats
 {
     uint64_t queries = 0, sphere_tests = 0, sphere_hits = 0, plane_tests = 0, merge_steps = 0, shaded = 0,
              refract_children = 0, scatter_children = 0, attempts = 0, draws = 0, leaf_children = 0;
+    uint64_t tex[7] = {0, 0, 0, 0, 0, 0, 0}; /* texture evaluations by class (TexCount) */
     void add(const Stats &o)
     {
+        for (int k = 0; k < 7; k++) tex[k] += o.tex[k];
         queries += o.queries, sphere_tests += o.sphere_tests, sphere_hits += o.sphere_hits;
         plane_tests += o.plane_tests, merge_steps += o.merge_steps, shaded += o.shaded;
         refract_children += o.refract_children, scatter_children += o.scatter_children;
@@ -1272,7 +1284,9 @@ int oracle_render_adaptive(const char *scene_text, int W, int H, int spp, int de
 
 
 /* stats[0..10]: queries sphere_tests sphere_hits plane_tests merge_steps shaded
- * refract_children scatter_children attempts draws leaf_children */
+ * refract_children scatter_children attempts draws leaf_children; stats[11..17]:
+ * texture evaluations (TexCount: xform multiply image spherical mirrorball
+ * skybox log) -- the caller's array holds 18 */
 int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int depth, float sw, float sh,
                      float dist, uint64_t seed, const int32_t *pixels, int npx, int threads, int order,
                      int per_sample, float *out, uint64_t *stats);
@@ -1298,6 +1312,7 @@ int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int 
         std::string err;
         auto worker = [&]() {
             Tracer<SampleEngine> tr(*scene, order == 1 ? ORDER_FAST : ORDER_REFERENCE);
+            for (uint64_t &c : tl_tex) c = 0;
             try {
                 for (;;) {
                     int k = next.fetch_add(1);
@@ -1326,6 +1341,7 @@ int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int 
                 err = e.what();
             }
             std::lock_guard<std::mutex> g(mu);
+            for (int c = 0; c < TC_N; c++) tr.st.tex[c] = tl_tex[c];
             total.add(tr.st);
         };
         std::vector<std::thread> pool;
@@ -1334,6 +1350,7 @@ int oracle_render_gw(const char *scene_text, int W, int H, int gw, int spp, int 
         if (!err.empty())
             throw std::runtime_error(err);
         if (stats) {
+            for (int c = 0; c < TC_N; c++) stats[11 + c] = total.tex[c];
             uint64_t v[11] = {total.queries,          total.sphere_tests,     total.sphere_hits, total.plane_tests,
                               total.merge_steps,      total.shaded,           total.refract_children,
                               total.scatter_children, total.attempts,         total.draws,

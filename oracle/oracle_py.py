@@ -24,7 +24,9 @@ ORDER_REFERENCE = 0
 ORDER_FAST = 1
 
 STAT_NAMES = ["queries", "sphere_tests", "sphere_hits", "plane_tests", "merge_steps", "shaded",
-              "refract_children", "scatter_children", "attempts", "draws", "leaf_children"]
+              "refract_children", "scatter_children", "attempts", "draws", "leaf_children",
+              # texture evaluations by class (oracle.cpp TexCount)
+              "tex_xform", "tex_multiply", "tex_image", "tex_spherical", "tex_mirrorball", "tex_skybox", "tex_log"]
 
 _lib = None
 
@@ -82,7 +84,7 @@ def render(scene_text: str, W: int, H: int, spp: int, depth: int, screen=None, s
     px = None if pixels is None else np.ascontiguousarray(np.asarray(pixels, dtype=np.int32))
     npx = W * H if px is None else len(px)
     out = np.zeros((npx, spp, 3) if per_sample else (npx, 3), dtype=np.float32)
-    st = np.zeros(16, dtype=np.uint64)
+    st = np.zeros(24, dtype=np.uint64)
     if threads <= 0:
         threads = os.cpu_count() or 1
     rc = L.oracle_render(scene_text.encode(), W, H, spp, depth, sw, sh, dist, seed,

@@ -38,6 +38,7 @@
 #include "../include/pt/pt_engine.h"
 #include "scene_text.h"
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -213,40 +214,59 @@ int mode_render(int argc, char **argv)
     std::string out = argv[14];
     size_t np = pixels.size();
     std::vector<float> result(per_sample ? np * (size_t)spp * 3 : np * 3);
-    std::atomic<size_t> next(0);
     std::atomic<unsigned long long> queries(0);
+    /* The pool deals (pixel, 32-sample block) units, not whole pixels: one
+     * pixel's 1024 samples on one thread made a bounded sample's few expensive
+     * pixels its tail.  Each unit keeps its samples' colours; a
+     * pixel's mean is then tracePixel's own sequential sum over them, so the
+     * bits are unchanged.  Pixels go in windows whose per-sample colours fit
+     * 256 MB. */
+    const int kBlock = 32;
+    const size_t nb = ((size_t)spp + kBlock - 1) / kBlock;
+    const size_t win = per_sample ? std::max<size_t>(np, 1)
+                                  : std::max<size_t>(1, ((size_t)256 << 20) / ((size_t)spp * 12));
+    std::vector<float> vals(per_sample ? 0 : std::min(win, np) * (size_t)spp * 3);
     auto t0 = std::chrono::steady_clock::now();
-    auto worker = [&]() {
-        CountingIterator it(w.root->makeSpanIterator());
-        for (;;) {
-            size_t k = next.fetch_add(1);
-            if (k >= np)
-                break;
-            int p = pixels[k], px = p % W, py = p / W;
-            Color acc(0, 0, 0);
-            for (int s = 0; s < spp; s++) {
-                PtSampleEngine e((uint64_t)seed, (uint64_t)p, (uint64_t)s);
-                Color c = tracePixel(it, px, py, W, H, 1, depth, sw, sh, dist, e);
-                if (per_sample) {
-                    float *o = &result[(k * spp + s) * 3];
+    for (size_t w0 = 0; w0 < np; w0 += win) {
+        const size_t wn = std::min(win, np - w0);
+        float *vb = per_sample ? &result[w0 * (size_t)spp * 3] : vals.data();
+        std::atomic<size_t> next(0);
+        auto worker = [&]() {
+            CountingIterator it(w.root->makeSpanIterator());
+            for (;;) {
+                const size_t u = next.fetch_add(1);
+                if (u >= wn * nb)
+                    break;
+                const size_t k = u / nb;
+                const int b = (int)(u % nb);
+                const int p = pixels[w0 + k], px = p % W, py = p / W;
+                for (int s = b * kBlock; s < spp && s < (b + 1) * kBlock; s++) {
+                    PtSampleEngine e((uint64_t)seed, (uint64_t)p, (uint64_t)s);
+                    Color c = tracePixel(it, px, py, W, H, 1, depth, sw, sh, dist, e);
+                    float *o = &vb[(k * spp + s) * 3];
                     o[0] = c.x;
                     o[1] = c.y;
                     o[2] = c.z;
                 }
-                acc += c;
             }
-            acc /= spp;
-            if (!per_sample) {
-                result[k * 3 + 0] = acc.x;
-                result[k * 3 + 1] = acc.y;
-                result[k * 3 + 2] = acc.z;
+            queries += it.queries;
+        };
+        std::vector<std::thread> pool;
+        for (int t = 0; t < threads; t++) pool.emplace_back(worker);
+        for (auto &t : pool) t.join();
+        if (!per_sample)
+            for (size_t k = 0; k < wn; k++) { /* tracePixel's spp loop: acc += c in sample order, / spp */
+                Color acc(0, 0, 0);
+                for (int s = 0; s < spp; s++) {
+                    const float *v = &vb[(k * spp + s) * 3];
+                    acc += Color(v[0], v[1], v[2]);
+                }
+                acc /= spp;
+                result[(w0 + k) * 3 + 0] = acc.x;
+                result[(w0 + k) * 3 + 1] = acc.y;
+                result[(w0 + k) * 3 + 2] = acc.z;
             }
-        }
-        queries += it.queries;
-    };
-    std::vector<std::thread> pool;
-    for (int t = 0; t < threads; t++) pool.emplace_back(worker);
-    for (auto &t : pool) t.join();
+    }
     double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     write_file(out, result.data(), result.size() * 4);
     printf("{\"seconds\": %.6f, \"samples\": %zu, \"queries\": %llu, \"threads\": %d}\n", secs, np * (size_t)spp,

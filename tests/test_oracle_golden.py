@@ -111,3 +111,26 @@ def test_config_golden_matches_oracle(built, tmp_path, name, npix):
     assert (W, H, spp, depth) == (cfg.width, cfg.height, cfg.spp, cfg.depth)
     got = O.render(to_text(cfg.scene(), str(tmp_path)), W, H, spp, depth, screen=cfg.screen, seed=seed, pixels=pix)
     np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_ref_render_block_units_same_bits(built):
+    """oracle/_ref/ptref's pool deals (pixel, 32-sample block) units since round 6
+    (the CPU baseline's tail): the pixel means are still
+    tracePixel's sequential sum -- equal to the restated oracle in reference
+    order and to the unit's own per-sample values summed in order."""
+    import oracle_py as O
+    from pathtrace import scenes
+    from pathtrace.scene import to_text
+    if not O.ref_available():
+        pytest.skip("oracle/_ref/ptref not built (no /root/reference)")
+    W, H, spp, depth = 32, 24, 70, 8  # 70 = two whole blocks and a ragged one
+    txt = to_text(scenes.scene_p1(), "/tmp/pt_test_refblocks")
+    pix = np.array([5, 100, 300, 301, 600, 767], np.int32)
+    got = O.ref_render(txt, W, H, spp, depth, pixels=pix, threads=5)
+    want = O.render(txt, W, H, spp, depth, pixels=pix, threads=2, order=O.ORDER_REFERENCE)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    per = O.ref_render(txt, W, H, spp, depth, pixels=pix, threads=3, per_sample=True)
+    acc = np.zeros((len(pix), 3), np.float32)
+    for s in range(spp):
+        acc = (acc + per[:, s]).astype(np.float32)
+    np.testing.assert_array_equal((acc / np.float32(spp)).view(np.uint32), got.view(np.uint32))
