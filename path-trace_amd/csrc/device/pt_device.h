@@ -751,7 +751,19 @@ struct Sph
     {
         const float b = dot(c.omc, q.d);
         const float disc = b * b - q.a * c.c;
+#if PT_RECEDE_DEAD
+        /* Union-only trees (codegen): a sphere the ray leaves from outside
+         * (c > 0, b >= 0) has t1 <= 0 -- fl(a*c) >= 0 makes disc <= fl(b*b),
+         * so sqrt(disc) <= b -- and a span ending before EPS changes no union
+         * result: the union rule never takes it, and in the lazy merge it can
+         * only join spans that start before EPS, whose ends (and end normals)
+         * it never supplies (src/union.cpp:84-134, path-trace.h:66-100).  Such
+         * a lane counts as dead, so a wave whose other lanes miss skips the
+         * root and the divisions. */
+        const bool live = !(disc <= EPS) && !(c.c > 0.0f && b >= 0.0f);
+#else
         const bool live = !(disc <= EPS);
+#endif
 #if PT_SPHERE_SKIP
         /* no lane meets the sphere: skip the root and the divisions (a dead
          * span's bounds are never read) */

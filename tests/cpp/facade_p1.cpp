@@ -63,7 +63,8 @@ inline V3 mk(float x, float y, float z)
     r.x = x, r.y = y, r.z = z;
     return r;
 }
-#define PT_TEXT(...) #__VA_ARGS__
+#define PT_TEXT_(...) #__VA_ARGS__
+#define PT_TEXT(...) PT_TEXT_(__VA_ARGS__) /* expands the body macro, then stringises it */
 #define CHECKER_BODY                                                                  \
     const float s = prm[0];                                                           \
     const float k = floorf(p.x * s) + floorf(p.y * s) + floorf(p.z * s);              \

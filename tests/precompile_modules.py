@@ -32,8 +32,9 @@ def test_jobs():
     jobs += [(lambda b=b, k=k: _queries(b, k), None) for b, n in zip(zoo.TEX_EVAL_SCENES, TEX_EVAL_COUNTS)
              for k in range(n)]
     # tests/test_user_texture.py, tests/test_facade.py: user Texture subclasses (pt_tex_device)
-    from test_user_texture import user_scene, facade_user_scene
-    jobs += [((lambda: pt.DeviceScene(user_scene())), 4), ((lambda: pt.DeviceScene(facade_user_scene())), 6)]
+    from test_user_texture import user_scene, facade_user_scene, CHECKER_FACADE
+    jobs += [((lambda: pt.DeviceScene(user_scene())), 4), ((lambda: pt.DeviceScene(facade_user_scene())), 6),
+             ((lambda: pt.DeviceScene(facade_user_scene(CHECKER_FACADE))), 6)]
     return jobs
 
 

@@ -25,6 +25,12 @@ CHECKER = """
     return odd != 0.0f ? mk(prm[1], prm[2], prm[3]) : mk(prm[4], prm[5], prm[6]);
 """
 CHECKER_PRM = (2.0, 1.0, 0.9, 0.3, 0.2, 0.3, 1.0)
+# the same body as tests/cpp/facade_p1.cpp's CheckerTexture hands the device
+# (its macro, expanded and stringised: one line), so build() can precompile
+# the facade binary's module too
+CHECKER_FACADE = ("const float s = prm[0]; const float k = floorf(p.x * s) + floorf(p.y * s) + floorf(p.z * s); "
+                  "const float odd = k - 2.0f * floorf(k * 0.5f); "
+                  "return odd != 0.0f ? mk(prm[1], prm[2], prm[3]) : mk(prm[4], prm[5], prm[6]);")
 # a getFloat override: a scatter coefficient that halves below y = -0.2
 BANDS_COLOR = "return mk(p.y, p.y * 0.5f, 0.25f);"
 BANDS_VALUE = "return p.y > -0.2f ? prm[0] : prm[0] * 0.5f;"
@@ -77,11 +83,11 @@ def user_scene(scatter=0.9):
                  Union(Sphere((0, .3, -5), .5, diffuse), Plane((0, 1, 0), .5, floor)))
 
 
-def facade_user_scene():
+def facade_user_scene(body=CHECKER):
     """tests/cpp/facade_p1.cpp `usertex`: the floor's emission its CheckerTexture"""
     diffuse = Material(ColorTexture(0.8), ColorTexture(1))
     mirror = Material(ColorTexture(0.99), ColorTexture(0))
-    floor = Material(ColorTexture(0), ColorTexture(0), DeviceTexture(CHECKER, CHECKER_PRM))
+    floor = Material(ColorTexture(0), ColorTexture(0), DeviceTexture(body, CHECKER_PRM))
     return Union(Union(Sphere((-1, 0, -4), .5, diffuse), Sphere((1, 0, -4), .5, mirror)),
                  Union(Sphere((0, .3, -5), .5, diffuse), Plane((0, 1, 0), .5, floor)))
 

@@ -7,7 +7,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 code = ("import sys; sys.path.insert(0, %r)\n"
         "import pathtrace as pt\nfrom pathtrace import scenes\n"
-        "pt.DeviceScene(scenes.scene_p1()).compile(8)\n") % os.path.join(ROOT, "path-trace_amd")
+        "scenes.CONFIGS[\"C3\"].device_scene().compile(8)\n") % os.path.join(ROOT, "path-trace_amd")
 procs = []
 for h in sys.argv[1:] or ["-"]:
     env = dict(os.environ)
