@@ -55,7 +55,7 @@ OPS_PER_QUERY = {"C3": 438.75, "C4": 438.75, "C2": 651.97, "C5": 679.78}
 # rocprofv3 --pmc passes of bench.py; VALUBusy, HBM bytes = FETCH_SIZE x 2 +
 # WRITE_SIZE).  Each file records the code-object key of the kernel its passes
 # ran; the line attaches it only when that key is the key of the kernel it timed.
-PMC_JSON = os.path.join(ROOT, "profiles", "round5", "pmc_bench_%s.json")
+PMC_JSON = os.path.join(ROOT, "profiles", "round6", "pmc_bench_%s.json")
 # bounded CPU samples at full spp on the box's per-GPU CPU share (16 threads):
 # BASELINE.md's 4096 hashed pixels (C3: ~60 s), fewer where a pixel costs more
 CPU_PIXELS = {"C1": 4096, "C2": 512, "C3": 4096, "C4": 1024, "C5": 32768}
@@ -251,11 +251,11 @@ def cpu_baseline(cfg, txt, spp, npix, threads, frame_qps, within=None):
            "sample_queries_per_sample": round(qps, 2)}
     scal = None
     try:  # the measured thread scaling of this baseline (tools/cpu_scaling.py on a GPU box)
-        with open(os.path.join(ROOT, "profiles", "round5", "cpu_scaling.json")) as f:
+        with open(os.path.join(ROOT, "profiles", "round6", "cpu_scaling.json")) as f:
             rows = json.load(f)["C3_sample_scaling"]["rows"]
         scal = {"threads": [r["threads"] for r in rows],
                 "parallel_efficiency": [round(r["parallel_efficiency"], 3) for r in rows],
-                "file": "profiles/round5/cpu_scaling.json"}
+                "file": "profiles/round6/cpu_scaling.json"}
     except (OSError, ValueError, KeyError):
         pass
     if scal:

@@ -477,7 +477,11 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 v)
     v += dpp_u32<0x143, 0xC>(v);
     return v;
 }
-/* (v << 1) | this lane's bit of the uniform mask m: one v_addc (v + v + carry-in m) */
+/* (v << 1) | this lane's bit of the uniform mask m: one v_addc (v + v + carry-in m).
+ * Each active lane's result depends on its own v and bit `lane` of m only, not
+ * on EXEC (the instruction writes nothing for inactive lanes, like any VALU
+ * op), so the compiler may move or merge it as a pure value.  The call site
+ * (the lane-major generation round) runs with all 64 lanes active. */
 __device__ __forceinline__ u32 shl_lane_bit(u32 v, u64 m)
 {
     u32 r;
@@ -752,7 +756,9 @@ struct Sph
         const float b = dot(c.omc, q.d);
         const float disc = b * b - q.a * c.c;
 #if PT_RECEDE_DEAD
-        /* Union-only trees (codegen): a sphere the ray leaves from outside
+        /* Experiment hook, off: exact, but C2 -4 % (the waves whose only live
+         * lanes recede are rare; profiles/round6/ab_recede_dead_c2_not_kept.txt).
+         * Union-only trees: a sphere the ray leaves from outside
          * (c > 0, b >= 0) has t1 <= 0 -- fl(a*c) >= 0 makes disc <= fl(b*b),
          * so sqrt(disc) <= b -- and a span ending before EPS changes no union
          * result: the union rule never takes it, and in the lazy merge it can
