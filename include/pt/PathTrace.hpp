@@ -689,15 +689,33 @@ public:
      * device: init(ray) runs pt_query_spans on this object's flattened copy and
      * next() walks the returned list (bit-identical to the reference's lazy
      * iterators, Difference quirk included).  A user-defined subclass
-     * overrides it as in the reference (host-only, not renderable). */
+     * overrides it as in the reference (host-side), and gets a device form --
+     * renders, device span queries -- when its iterator yields one span per
+     * ray and it returns that span's arithmetic as device source
+     * (deviceSpan / deviceNormal below, pt_object_device). */
     inline virtual SpanIterator *makeSpanIterator() const;
     virtual Object *transform(const Matrix &) const { return nullptr; }
     virtual Object *duplicate() const = 0;
-    virtual pt_id flatten(Flattener &) const
-    {
-        throw DeviceError(PT_ERR_ARG, "a user-defined Object subclass has no device form");
-    }
+    /* The device form of a user-defined subclass: the bodies of
+     * bool span(V3 o, V3 d, float &t0, float &t1) and V3 normal(V3 p) over
+     * its parameters `const float *prm` (deviceParams), and its material. */
+    virtual const char *deviceSpan() const { return nullptr; }
+    virtual const char *deviceNormal() const { return nullptr; }
+    virtual std::vector<float> deviceParams() const { return std::vector<float>(); }
+    virtual const Material *deviceMaterial() const { return nullptr; }
+    inline virtual pt_id flatten(Flattener &f) const;
 };
+
+inline pt_id Object::flatten(Flattener &f) const
+{
+    const char *sp = deviceSpan(), *nb = deviceNormal();
+    if (!sp || !nb || !deviceMaterial())
+        throw DeviceError(PT_ERR_ARG, "a user-defined Object subclass has no device form "
+                                      "(override deviceSpan, deviceNormal and deviceMaterial)");
+    const std::vector<float> prm = deviceParams();
+    return ptCheck(pt_object_device(f.s, sp, nb, prm.data(), (int)prm.size(), f.material(deviceMaterial())));
+}
+
 
 /* The device-served SpanIterator of a built-in object (one query per init). */
 class DeviceSpanIterator : public SpanIterator

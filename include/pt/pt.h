@@ -111,6 +111,25 @@ pt_id pt_plane_through(pt_scene *s, float nx, float ny, float nz,               
 #define PT_CSG_DIFFERENCE 2   /* Difference   difference.h:12   */
 pt_id pt_csg(pt_scene *s, int op, pt_id a, pt_id b);
 pt_id pt_transformed(pt_scene *s, const float m[12], pt_id child);             /* TransformedObject object.h:78 */
+/* A user-defined Object subclass (include/object.h:10-24: the virtual
+ * makeSpanIterator) whose iterator yields at most one span per ray -- a convex
+ * shape -- as device source, compiled into the scene's modules
+ * (path-trace_amd/csrc/device/pt_user_object.h).  span_body is the body of
+ *     bool span(V3 o, V3 d, float &t0, float &t1)
+ * returning whether the ray o + t d (d not normalised) meets the object, and
+ * then its entry and exit parameters t0 <= t1 (the Span's start and end,
+ * include/span.h); normal_body is the body of
+ *     V3 normal(V3 p)
+ * returning the outward surface normal at p, which is the span's start normal
+ * at the entry point and its end normal at the exit.  Both read the nparams
+ * parameters as `const float *prm` and use the device library's vocabulary
+ * (V3, mk, dot, normalize, the f32 math builtins), compiled without FMA
+ * contraction and with correctly rounded '/' and sqrt, so they compute what
+ * the same text compiled on the host with -ffp-contract=off computes.  The
+ * object takes part in every CSG node and transform like a built-in
+ * primitive; the kernel's fast paths treat it conservatively (never dark). */
+pt_id pt_object_device(pt_scene *s, const char *span_body, const char *normal_body, const float *params,
+                       int nparams, pt_id mat);
 int pt_set_root(pt_scene *s, pt_id obj);
 /* Load a whole scene from the plain-text scene format (oracle/scene_text.h
  * documents it; pathtrace.scene.to_text writes it).  Replaces the current

@@ -553,6 +553,48 @@ struct SphereNode : Node /* src/sphere.cpp:6-49 */
     }
 };
 
+/* A user-defined Object subclass with one span per ray (pt_object_device):
+ * the host functions a test registered for its slot (the same source the
+ * product compiles into the device module, built with -ffp-contract=off). */
+typedef int (*user_span_fn)(const float *o, const float *d, const float *prm, float *t01);
+typedef void (*user_normal_fn)(const float *p, const float *prm, float *n);
+struct UserObjFns
+{
+    user_span_fn span = nullptr;
+    user_normal_fn normal = nullptr;
+};
+std::map<int, UserObjFns> &user_obj_slots()
+{
+    static std::map<int, UserObjFns> m;
+    return m;
+}
+struct UserNode : Node
+{
+    UserObjFns fn;
+    std::vector<float> prm;
+    const Material *m;
+    V3 normal(V3 p) const
+    {
+        const float q[3] = {p.x, p.y, p.z};
+        float n[3];
+        fn.normal(q, prm.data(), n);
+        return V3(n[0], n[1], n[2]);
+    }
+    void spans(const Ray &r, SpanList &out, Stats &) const override
+    {
+        const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+        float t[2];
+        if (!fn.span(o, d, prm.data(), t))
+            return;
+        Span sp;
+        sp.t0 = t[0], sp.t1 = t[1];
+        sp.n0 = normal(r.at(sp.t0));
+        sp.n1 = normal(r.at(sp.t1));
+        sp.m0 = sp.m1 = m;
+        out.push(sp);
+    }
+};
+
 struct PlaneNode : Node /* src/plane.cpp:23-63: half-space {p : n.p + d < 0} */
 {
     V3 n;
@@ -829,6 +871,17 @@ std::unique_ptr<Node> make_node(const scenetext::Desc &d, Scene &s, int id)
         auto p = new PlaneNode;
         p->n = V3(o.f[0], o.f[1], o.f[2]);
         p->d = o.f[3];
+        p->m = s.mats.at(o.i[0]).get();
+        return std::unique_ptr<Node>(p);
+    }
+    if (o.type == "user") {
+        auto it = user_obj_slots().find(o.i[1]);
+        if (it == user_obj_slots().end() || !it->second.span || !it->second.normal)
+            throw std::runtime_error("oracle: no host functions registered for user object slot " +
+                                     std::to_string(o.i[1]));
+        auto p = new UserNode;
+        p->fn = it->second;
+        p->prm = o.f;
         p->m = s.mats.at(o.i[0]).get();
         return std::unique_ptr<Node>(p);
     }
@@ -1126,6 +1179,15 @@ using namespace oracle;
 extern "C" {
 
 const char *oracle_last_error() { return g_err.c_str(); }
+
+/* test infrastructure: the host functions of user object slot `slot` */
+int oracle_register_user_object(int slot, user_span_fn span, user_normal_fn normal)
+{
+    if (!span || !normal)
+        return -1;
+    user_obj_slots()[slot] = UserObjFns{span, normal};
+    return 0;
+}
 
 /* test infrastructure: the host functions of user texture slot `slot` (value may be NULL) */
 int oracle_register_user_texture(int slot, user_color_fn color, user_value_fn value)

@@ -67,6 +67,8 @@ def lib():
         L.oracle_trace_rays.restype = C.c_int
         L.oracle_trace_rays.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int,
                                         C.c_int64, C.c_int, C.c_int, C.c_void_p]
+        L.oracle_register_user_object.restype = ctypes.c_int
+        L.oracle_register_user_object.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_register_user_texture.restype = ctypes.c_int
         L.oracle_register_user_texture.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_kat.restype = ctypes.c_int
@@ -231,6 +233,15 @@ def ref_render(scene_text: str, W: int, H: int, spp: int, depth: int, screen=Non
     if info:
         return res, json.loads(out.strip().splitlines()[-1])
     return res
+
+
+def register_user_object(slot: int, span_fn: int, normal_fn: int) -> None:
+    """Test infrastructure: the host functions (addresses of
+    int span(const float *o, const float *d, const float *prm, float *t01) and
+    void normal(const float *p, const float *prm, float *n)) the oracle calls
+    for `obj <id> user <slot> ...` records (pathtrace.scene.DeviceObject)."""
+    if lib().oracle_register_user_object(int(slot), span_fn, normal_fn) != 0:
+        raise RuntimeError("oracle_register_user_object: null function")
 
 
 def register_user_texture(slot: int, color_fn: int, value_fn: int = 0) -> None:

@@ -28,6 +28,8 @@
  *   obj <id> plane <nx> <ny> <nz> <d> <mat>              Plane    src/plane.cpp:6-9
  *   obj <id> union|intersection|difference <a> <b>       src/{union,intersection,difference}.cpp
  *   obj <id> xform <12 f> <child>                        TransformedObject include/object.h:26-98
+ *   obj <id> user <slot> <mat> <n> <n f>                 a user Object subclass: the host functions
+ *                                                        registered for <slot> (oracle_register_user_object)
  *   root <id>
  *
  * Matrices use the reference constructor order (x00 x10 x20 x30 x01 ... x32),
@@ -173,6 +175,12 @@ inline Desc parse(const std::string &text)
                 need(16);
                 for (int k = 3; k < 15; k++) it.f.push_back(parse_float(tok[k]));
                 it.i = {parse_int(tok[15])};
+            } else if (ty == "user") {
+                if (tok.size() < 6)
+                    throw std::runtime_error("scene_text: wrong operand count in '" + line + "'");
+                it.i = {parse_int(tok[4]), parse_int(tok[3]), parse_int(tok[5])}; /* mat, slot, n */
+                need(6 + (size_t)it.i[2]);
+                for (size_t k = 6; k < tok.size(); k++) it.f.push_back(parse_float(tok[k]));
             } else
                 throw std::runtime_error("scene_text: unknown object " + ty);
             d.objects.push_back(it);

@@ -21,23 +21,24 @@ HEADERS = ["internal.h", "device/pt_device.h", "../../include/pt/pt.h", "../../i
 
 
 def _embed_device_header() -> None:
-    with open(os.path.join(CSRC, "device", "pt_device.h")) as f:
-        text = f.read()
-    if ")PTDEV\"" in text:
-        raise RuntimeError("device header contains the raw-string delimiter")
-    out = 'R"PTDEV(' + text + ')PTDEV"\n'
-    path = os.path.join(CSRC, "pt_device_src.inc")
-    old = open(path).read() if os.path.exists(path) else None
-    if old != out:
-        with open(path, "w") as f:
-            f.write(out)
+    for name, inc in (("pt_device.h", "pt_device_src.inc"), ("pt_user_object.h", "pt_user_object_src.inc")):
+        with open(os.path.join(CSRC, "device", name)) as f:
+            text = f.read()
+        if ")PTDEV\"" in text:
+            raise RuntimeError("device header contains the raw-string delimiter")
+        out = 'R"PTDEV(' + text + ')PTDEV"\n'
+        path = os.path.join(CSRC, inc)
+        old = open(path).read() if os.path.exists(path) else None
+        if old != out:
+            with open(path, "w") as f:
+                f.write(out)
 
 
 def _stale() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = SOURCES + HEADERS + ["pt_device_src.inc"]
+    deps = SOURCES + HEADERS + ["pt_device_src.inc", "pt_user_object_src.inc"]
     return any(os.path.getmtime(os.path.join(CSRC, d)) > t for d in deps)
 
 

@@ -6,6 +6,7 @@
  * virtual calls (SpanIterator::init/next, Texture::getColor/getFloat) thus
  * turn into straight-line, fully inlined code per scene.
  */
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -37,6 +38,7 @@ struct Gen
     int unit_axis[3] = {0, 0, 0}; /* planes with normal +-e_k outside transforms */
     std::vector<std::pair<size_t, int>> unit_planes; /* (position of the ",U" mark in a node string, axis) */
     std::map<int, int> user_tex; /* User texture id -> offset of its parameters in P */
+    std::vector<int> user_obj;   /* User objects reached (their bodies become UObjB_<id>) */
 
     explicit Gen(const SceneImpl &sc) : s(sc) {}
 
@@ -117,6 +119,14 @@ struct Gen
             std::string a = obj(o.a);
             std::string b = obj(o.b);
             t << n << "<" << a << "," << b << ">";
+            break;
+        }
+        case ObjKind::User: {
+            const int off = (int)P.size();
+            P.insert(P.end(), o.params.begin(), o.params.end());
+            if (std::find(user_obj.begin(), user_obj.end(), id) == user_obj.end())
+                user_obj.push_back(id);
+            t << "UObj<" << prim++ << "," << off << "," << material(o.mat) << ",UObjB_" << id << ">";
             break;
         }
         case ObjKind::Xform: {
@@ -220,6 +230,18 @@ struct Gen
     std::string user_defs() const
     {
         std::ostringstream d;
+        for (int id : user_obj) {
+            const ObjRec &o = s.objects.at(id);
+            d << "struct UObjB_" << id << " {\n"
+              << "  __device__ static __forceinline__ bool span(V3 o, V3 d, const float *prm, float &t0, float &t1) {\n"
+              << "    (void)prm;\n"
+              << "#line 1 \"pt_object_device " << id << " span\"\n"
+              << o.span_body << "\n  }\n"
+              << "  __device__ static __forceinline__ V3 normal(V3 p, const float *prm) {\n"
+              << "    (void)prm;\n"
+              << "#line 1 \"pt_object_device " << id << " normal\"\n"
+              << o.normal_body << "\n  }\n};\n";
+        }
         for (const auto &u : user_tex) {
             const TexRec &x = s.textures.at(u.first);
             d << "struct UTex_" << u.first << " {\n"
@@ -361,6 +383,8 @@ Generated generate(const SceneImpl &s, int depth, bool rays)
     } else {
         src << device_library_source() << "\n";
     }
+    if (!g.user_obj.empty())
+        src << device_user_object_source() << "\n";
     src << "namespace ptgen {\nusing namespace ptd;\n";
     src << g.user_defs();
     src << "typedef " << root << " RootT;\n";
@@ -444,6 +468,8 @@ Generated generate_query(const SceneImpl &s, int obj, int tex)
         src << "#define PT_AXIS_SHARE " << axis_share << "\n";
     const std::string qtex = tex >= 0 ? g.tex(tex) : std::string();
     src << device_library_source() << "\n";
+    if (!g.user_obj.empty())
+        src << device_user_object_source() << "\n";
     src << "namespace ptgen {\nusing namespace ptd;\n";
     src << g.user_defs();
     if (obj >= 0)

@@ -12,4 +12,11 @@ std::string device_library_source()
         ;
     return src;
 }
+std::string device_user_object_source()
+{
+    static const char src[] =
+#include "pt_user_object_src.inc"
+        ;
+    return src;
+}
 } // namespace pt

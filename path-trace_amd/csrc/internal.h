@@ -50,7 +50,7 @@ struct MatRec
     float ior;
 };
 
-enum class ObjKind { Sphere, Plane, Union, Intersection, Difference, Xform };
+enum class ObjKind { Sphere, Plane, Union, Intersection, Difference, Xform, User };
 
 struct ObjRec
 {
@@ -58,6 +58,9 @@ struct ObjRec
     float f[12] = {0}; /* sphere: c, r; plane: n, d; xform: m */
     int mat = -1;
     int a = -1, b = -1; /* children */
+    /* User (pt_object_device): the caller's device bodies and parameters */
+    std::string span_body, normal_body;
+    std::vector<float> params;
 };
 
 struct DeviceState; /* runtime.cpp */
@@ -129,6 +132,7 @@ void write_hdr(const std::string &path, const float *rgb, int w, int h);
 void write_bmp(const std::string &path, const float *rgb, int w, int h, int count);
 
 std::string device_library_source(); /* embedded pt_device.h */
+std::string device_user_object_source(); /* embedded pt_user_object.h (scenes with user objects) */
 
 } // namespace pt
 

@@ -704,6 +704,10 @@ std::shared_ptr<const Generated> generated(SceneImpl &s, int depth, bool rays)
     for (const ObjRec &o : s.objects) {
         f.add(o.kind), f.add(o.mat), f.add(o.a), f.add(o.b);
         f.bytes(o.f, sizeof o.f);
+        f.str(o.span_body.c_str()), f.str(o.normal_body.c_str());
+        f.add(o.params.size());
+        if (!o.params.empty())
+            f.bytes(o.params.data(), o.params.size() * sizeof(float));
     }
     f.add(s.objects.size());
     for (const MatRec &m : s.materials) {
@@ -1393,6 +1397,30 @@ pt_id pt_transformed(pt_scene *s, const float m[12], pt_id child)
         o.kind = ObjKind::Xform;
         memcpy(o.f, m, 48);
         o.a = child;
+        sc.objects.push_back(o);
+        return (int)sc.objects.size() - 1;
+    });
+}
+
+/* A user-defined Object subclass (include/object.h:10-24: the virtual
+ * makeSpanIterator) with one span per ray, as device source compiled into the
+ * scene's modules (device/pt_user_object.h). */
+pt_id pt_object_device(pt_scene *s, const char *span_body, const char *normal_body, const float *params,
+                       int nparams, pt_id mat)
+{
+    return guard([&] {
+        SceneImpl &sc = S(s);
+        if (!span_body || !*span_body || !normal_body || !*normal_body)
+            throw Error(PT_ERR_ARG, "pt_object_device: empty span or normal body");
+        if (nparams < 0 || nparams > (1 << 16) || (nparams > 0 && !params))
+            throw Error(PT_ERR_ARG, "pt_object_device: bad parameter block");
+        check_mat(sc, mat);
+        ObjRec o;
+        o.kind = ObjKind::User;
+        o.mat = mat;
+        o.span_body = span_body;
+        o.normal_body = normal_body;
+        o.params.assign(params, params + nparams);
         sc.objects.push_back(o);
         return (int)sc.objects.size() - 1;
     });

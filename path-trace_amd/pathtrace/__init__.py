@@ -20,7 +20,7 @@ import numpy as np
 from . import _lib
 from ._lib import PT_ORDER_FAST, PT_ORDER_REFERENCE, PtError, RenderParams, RenderStats, TraceParams, load_hdr, \
     load_png, write_bmp, write_hdr
-from .scene import (ColorTexture, CoordTexture, DeviceTexture, Difference, Image, ImageAlphaTexture, ImageSkyboxAlphaTexture,
+from .scene import (ColorTexture, CoordTexture, DeviceObject, DeviceTexture, Difference, Image, ImageAlphaTexture, ImageSkyboxAlphaTexture,
                     ImageSkyboxTexture, ImageTexture, Intersection, LogTexture, Material, Matrix,
                     MirrorBallSkymapTexture, MultiplyTexture, Object, Plane, SphericalCoordinatesSkymapTexture,
                     Sphere, Texture, TransformedObject, TransformedTexture, Union, invert, to_text,
@@ -136,6 +136,10 @@ class DeviceScene:
             return c(L.pt_sphere(h, *[float(v) for v in o.center], float(o.r), self._material(o.material)))
         if isinstance(o, Plane):
             return c(L.pt_plane(h, *[float(v) for v in o.normal], float(o.d), self._material(o.material)))
+        if isinstance(o, DeviceObject):
+            prm = (ctypes.c_float * max(1, len(o.params)))(*o.params)
+            return c(L.pt_object_device(h, o.span_body.encode(), o.normal_body.encode(), prm, len(o.params),
+                                        self._material(o.material)))
         if isinstance(o, (Union, Intersection, Difference)):
             op = {Union: 0, Intersection: 1, Difference: 2}[type(o)]
             a = self._obj(o.a)

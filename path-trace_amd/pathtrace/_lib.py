@@ -82,6 +82,7 @@ SIGNATURES = {
     "pt_tex_transformed": (_I, [_P, _FP, _I]),
     "pt_tex_coord": (_I, [_P]),
     "pt_tex_device": (_I, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), _I]),
+    "pt_object_device": (_I, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_float), _I, _I]),
     "pt_material": (_I, [_P, _I, _I, _I, _I, _F, _I]),
     "pt_sphere": (_I, [_P, _F, _F, _F, _F, _I]),
     "pt_plane": (_I, [_P, _F, _F, _F, _F, _I]),

@@ -319,6 +319,26 @@ class Sphere(Object):
         return Sphere(self.center, self.r, self.material)
 
 
+class DeviceObject(Object):
+    """A user-defined Object subclass (reference include/object.h:10-24) with
+    one span per ray, given as device source (pt_object_device): `span_body`
+    is the body of bool span(V3 o, V3 d, float &t0, float &t1), `normal_body`
+    the body of V3 normal(V3 p); both read `params` as `const float *prm`.
+    `oracle_slot` names the host functions the CPU oracle calls for it
+    (oracle_py.register_user_object, test infrastructure)."""
+    kind = "user"
+
+    def __init__(self, span_body: str, normal_body: str, params, material: Material, oracle_slot: int = 0):
+        self.span_body = span_body
+        self.normal_body = normal_body
+        self.params = [float(v) for v in params]
+        self.material = material
+        self.oracle_slot = int(oracle_slot)
+
+    def duplicate(self):
+        return DeviceObject(self.span_body, self.normal_body, self.params, self.material, self.oracle_slot)
+
+
 class Plane(Object):
     """Half-space {p : normal.p + d < 0} (src/plane.cpp:23-63).  Plane(n, d, m)
     or Plane(n, point, m) with d = -dot(n, point) (src/plane.cpp:11-14)."""
@@ -455,6 +475,9 @@ class _Registry:
             args = "%s %s %s %s %d" % (*(_hex(c) for c in o.center), _hex(o.r), self.material(o.material))
         elif isinstance(o, Plane):
             args = "%s %s %s %s %d" % (*(_hex(c) for c in o.normal), _hex(o.d), self.material(o.material))
+        elif isinstance(o, DeviceObject):  # the oracle's host functions for the slot, the material, the parameters
+            args = "%d %d %d %s" % (o.oracle_slot, self.material(o.material), len(o.params),
+                                    " ".join(_hex(v) for v in o.params))
         elif isinstance(o, _Binary):
             a = self.obj(o.a)
             b = self.obj(o.b)

@@ -90,6 +90,38 @@ private:
     std::vector<float> prm_;
 };
 
+/* A user-defined Object subclass (include/object.h:10-24) with the
+ * reference sphere's arithmetic (src/sphere.cpp:31-49) as its device form:
+ * P1 built with it in place of one of its spheres renders P1's frame. */
+class UserSphere : public Object
+{
+public:
+    UserSphere(Vector3D c, float r, const Material *m) : c_(c), r_(r), m_(m) {}
+    Object *duplicate() const override { return new UserSphere(c_, r_, m_); }
+    const char *deviceSpan() const override
+    {
+        return "const V3 oc = mk(o.x - prm[0], o.y - prm[1], o.z - prm[2]);"
+               "const float a = dot(d, d), b = dot(oc, d), c = dot(oc, oc) - prm[3];"
+               "const float disc = b * b - a * c;"
+               "if (disc <= 1e-3f) return false;"
+               "const float s = sqrtf(disc);"
+               "t0 = (-b - s) / a; t1 = (-b + s) / a; return true;";
+    }
+    const char *deviceNormal() const override
+    {
+        return "const V3 q = mk(p.x - prm[0], p.y - prm[1], p.z - prm[2]);"
+               "float m = sqrtf(dot(q, q)); if (m == 0.0f) m = 1.0f;"
+               "return mk(q.x / m, q.y / m, q.z / m);";
+    }
+    std::vector<float> deviceParams() const override { return {c_.x, c_.y, c_.z, r_ * r_}; }
+    const Material *deviceMaterial() const override { return m_; }
+
+private:
+    Vector3D c_;
+    float r_;
+    const Material *m_;
+};
+
 int main(int argc, char **argv)
 {
     if (argc < 2)
@@ -455,6 +487,27 @@ int main(int argc, char **argv)
         Renderer renderer(world.get());
         if (!strcmp(argv[1], "key") && argc == 3) {
             printf("%s\n", pt_scene_kernel_key(renderer.handle(), atoi(argv[2])));
+            return 0;
+        }
+        if (!strcmp(argv[1], "userobj") && argc == 7) {
+            /* P1 with its glass sphere (1, 0, -4) a UserSphere */
+            Object *l = new Difference(new Union(new Sphere(Vector3D(-1, 0, -4), .6f, &diffuse),
+                                                 new Sphere(Vector3D(-.5f, 0, -4), .6f, &diffuse)),
+                                       new Sphere(Vector3D(-.7f, .3f, -3.6f), .4f, &diffuse));
+            Object *r = new Difference(new Union(new UserSphere(Vector3D(1, 0, -4), .6f, &glass),
+                                                 new Sphere(Vector3D(1.4f, .2f, -4.2f), .5f, &mirror)),
+                                       new Sphere(Vector3D(1, 0, -3.4f), .3f, &glass));
+            std::unique_ptr<Object> w(new Union(l, new Union(r, new Plane(Vector3D(0, 0, 1), 200, &sky))));
+            Renderer ur(w.get());
+            Renderer::Settings st;
+            st.width = atoi(argv[2]), st.height = atoi(argv[3]);
+            st.sampleCount = atoi(argv[4]), st.rayDepth = atoi(argv[5]);
+            std::vector<Color> img = ur.render(st);
+            FILE *f = fopen(argv[6], "wb");
+            if (!f)
+                return 5;
+            fwrite(img.data(), sizeof(Color), img.size(), f);
+            fclose(f);
             return 0;
         }
         if (!strcmp(argv[1], "render") && argc == 7) {

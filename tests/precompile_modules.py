@@ -35,6 +35,10 @@ def test_jobs():
     from test_user_texture import user_scene, facade_user_scene, CHECKER_FACADE
     jobs += [((lambda: pt.DeviceScene(user_scene())), 4), ((lambda: pt.DeviceScene(facade_user_scene())), 6),
              ((lambda: pt.DeviceScene(facade_user_scene(CHECKER_FACADE))), 6)]
+    # tests/test_user_object.py: user Object subclasses (pt_object_device)
+    from test_user_object import p0, box_scene
+    jobs += [((lambda: pt.DeviceScene(p0(True))), 6), ((lambda: pt.DeviceScene(p0(False))), 6),
+             ((lambda: pt.DeviceScene(box_scene())), 6), ((lambda: pt.DeviceScene(box_scene()).compile_queries()), None)]
     return jobs
 
 

@@ -181,3 +181,18 @@ def test_facade_user_texture_bitexact(facade_bin, tmp_path):
     got = np.fromfile(out, dtype=np.float32).reshape(-1, 3)
     want = pt.render(facade_user_scene(), W, H, spp, depth).reshape(-1, 3)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_facade_user_object_bitexact(facade_bin, tmp_path):
+    """A C++ Object subclass whose device form is the reference sphere's
+    arithmetic (deviceSpan / deviceNormal, pt_object_device), put in place of
+    one of P1's spheres: the frame is P1's bit for bit."""
+    W, H, spp, depth = 40, 24, 4, 8
+    out = str(tmp_path / "img.bin")
+    r = subprocess.run([facade_bin, "userobj", str(W), str(H), str(spp), str(depth), out],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.returncode, r.stderr)
+    got = np.fromfile(out, dtype=np.float32).reshape(-1, 3)
+    want = pt.render(scenes.scene_p1(), W, H, spp, depth).reshape(-1, 3)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
