@@ -203,10 +203,13 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
  * for k < n: */
 #define PT_PROF_TOTAL 0   /* the whole call                                                   */
 #define PT_PROF_SETUP 1   /* validation, the scene's generated module (cached), device buffers */
-#define PT_PROF_ENQUEUE 2 /* pixel upload, counter reset, render + reduce launches (with
-                             stats: also the wait for their timing events)                   */
-#define PT_PROF_WAIT 3    /* stream synchronise: the kernels' remaining run time              */
-#define PT_PROF_D2H 4     /* the result's copy to host memory                                 */
+#define PT_PROF_ENQUEUE 2 /* pixel upload, counter reset, render + reduce launches, the
+                             result's copy-back (with stats: also the wait for the
+                             launches' timing events)                                       */
+#define PT_PROF_WAIT 3    /* stream synchronise: the kernels' remaining run time and the
+                             copy-back (results up to 4 MB: a DMA into pinned staging)       */
+#define PT_PROF_D2H 4     /* the result into the caller's memory (pinned staging: a memcpy;
+                             larger results: a synchronous device-to-host copy)              */
 #define PT_PROF_KERNEL 5  /* render launch(es) by HIP events (0 unless stats were asked for,
                              or PT_CALL_KERNEL_TIME is set)                                   */
 #define PT_PROF_REDUCE 6  /* pt_reduce by HIP events (the same condition)                     */

@@ -113,6 +113,30 @@ struct DevBuf
     }
 };
 
+/* Page-locked host staging (grow-only): transfers from and to it are true
+ * DMA, with no driver-side staging copy (pt_render's small per-call transfers) */
+template <class T>
+struct PinBuf
+{
+    T *p = nullptr;
+    size_t n = 0;
+    void ensure(size_t count)
+    {
+        if (count <= n)
+            return;
+        release();
+        HIPCHECK(hipHostMalloc((void **)&p, count * sizeof(T), hipHostMallocDefault));
+        n = count;
+    }
+    void release()
+    {
+        if (p)
+            (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
 /* The HIP events and sample count of one render whose timings are not read yet */
 struct PendingRender
 {
@@ -141,6 +165,8 @@ struct DeviceState
     DevBuf<uint64_t> jump;
     DevBuf<float> stage, accum, fb;
     DevBuf<float> out; /* pt_render's output (grow-only: no allocation per call) */
+    PinBuf<int> hpix;  /* pt_render's pixel list and result, staged in pinned memory */
+    PinBuf<float> hout;
     DevBuf<int> pixels;
     DevBuf<uint64_t> stats;
     std::vector<PendingRender> pending; /* deferred timings (pt_render_device_timed) */
@@ -151,7 +177,7 @@ struct DeviceState
             for (auto &pr : pending)
                 for (auto e : pr.evs) (void)hipEventDestroy(e);
             P.release(), imgs.release(), jump.release(), stage.release(), accum.release(), fb.release();
-            out.release();
+            out.release(), hpix.release(), hout.release();
             pixels.release(), stats.release();
             for (auto &b : img_data) b.release();
             if (mod)
@@ -1566,6 +1592,8 @@ int pt_render_collect(pt_scene *s, int device, pt_render_stats *stats)
     });
 }
 
+constexpr size_t kPinFloats = (size_t)1 << 20; /* results up to 4 MB go through pinned staging */
+
 int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_stats *stats)
 {
     const double t0 = now_us();
@@ -1582,17 +1610,34 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
         std::shared_ptr<const Generated> gp;
         DeviceState &ds = prepare(sc, p, gp, false);
         ds.out.ensure(n);
+        const size_t nout = p->pixels ? (size_t)p->npixels * 3 : n;
+        /* small calls (a pixel, a block) stage the pixel list and the result in
+         * pinned memory: asynchronous DMA both ways and one synchronisation */
+        const bool pin = nout <= kPinFloats;
+        pt_render_params q = *p;
+        if (pin && p->pixels && p->npixels > 0) {
+            ds.hpix.ensure((size_t)p->npixels);
+            memcpy(ds.hpix.p, p->pixels, (size_t)p->npixels * 4);
+            q.pixels = ds.hpix.p;
+        }
+        if (pin)
+            ds.hout.ensure(std::max<size_t>(nout, 1));
         const double t1 = now_us();
         /* without stats the launches carry no events and no counter read-back */
         pt_render_stats local;
         const bool want = stats != nullptr || getenv("PT_CALL_KERNEL_TIME");
-        render_device(sc, p, ds.out.p, nullptr, stats ? stats : &local, want ? Timing::Sync : Timing::None, true);
+        render_device(sc, &q, ds.out.p, nullptr, stats ? stats : &local, want ? Timing::Sync : Timing::None, true);
+        if (pin && nout)
+            HIPCHECK(hipMemcpyAsync(ds.hout.p, ds.out.p, nout * 4, hipMemcpyDeviceToHost, nullptr));
         const double t2 = now_us();
         HIPCHECK(hipStreamSynchronize(nullptr));
         const double t3 = now_us();
-        const size_t nout = p->pixels ? (size_t)p->npixels * 3 : n;
-        if (nout)
-            HIPCHECK(hipMemcpy(rgb_out, ds.out.p, nout * 4, hipMemcpyDeviceToHost));
+        if (nout) {
+            if (pin)
+                memcpy(rgb_out, ds.hout.p, nout * 4);
+            else
+                HIPCHECK(hipMemcpy(rgb_out, ds.out.p, nout * 4, hipMemcpyDeviceToHost));
+        }
         const double t4 = now_us();
         g_prof[PT_PROF_SETUP] = t1 - t0;
         g_prof[PT_PROF_ENQUEUE] = t2 - t1;
