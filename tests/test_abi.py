@@ -129,3 +129,23 @@ def test_config_scenes_compile_for_gfx950(built, name):
     cfg = scenes.CONFIGS[name]
     key = cfg.device_scene().compile(cfg.depth)
     assert re.fullmatch(r"[0-9a-f]{16}", key)
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(width=0), "positive"), (dict(spp=0), "positive"), (dict(depth=65), "depth"),
+    (dict(spp=1 << 20), "spp must be"), (dict(sample_begin=-1), "samples must lie"),
+    (dict(sample_begin=(1 << 20) - 2, spp=4), "samples must lie"), (dict(order="sideways"), None),
+    (dict(pixels=[0, 5, 16 * 12]), "out of range"), (dict(pixels=[-1]), "out of range"),
+])
+def test_render_params_are_validated_before_device_work(built, kw, msg):
+    """pt_render refuses bad parameters with PT_ERR_ARG before it touches a device
+    (so this runs without one): the reference would assert or misbehave"""
+    import pathtrace as pt
+    from pathtrace import scenes
+    args = dict(width=16, height=12, spp=2, depth=4)
+    args.update(kw)
+    ds = pt.DeviceScene(scenes.scene_p0())
+    with pytest.raises((pt.PtError, KeyError, ValueError)) as ei:
+        pt.render(ds, args.pop("width"), args.pop("height"), args.pop("spp"), args.pop("depth"), **args)
+    if msg:
+        assert msg in str(ei.value)
