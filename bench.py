@@ -98,6 +98,8 @@ def parse():
                     help="0 = the CPUs this process may run on (sched_getaffinity), capped by OMP_NUM_THREADS "
                          "when set (the GPU box exports its per-GPU CPU share there)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-at-n", action="store_true",
+                    help="N > 1: also run the CPU baseline and the RMSE on rank 0 (default: the N = 1 line only)")
     ap.add_argument("--dump-frame", default="", help="rank 0: save the reduced frame (H x W x 3 f32 .npy)")
     ap.add_argument("--order", default="fast")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
@@ -372,8 +374,14 @@ def main():
     kernel_ms = st["kernel_ms"] / max(1, st["launches"])
     launches_per_step = st["launches"] // max(1, args.steps)
     queries = st["queries"]
+    per_rank = None
     if dist is not None:  # RCCL: CUDA tensors; gloo: host tensors
         dev = "cpu" if gloo else "cuda"
+        # every rank's own numbers first (the line reports the spread), then the max / sum
+        mine_t = torch.tensor([elapsed, kernel_ms, float(len(mine)), float(queries)], dtype=torch.float64, device=dev)
+        gathered = [torch.zeros_like(mine_t) for _ in range(world)]
+        dist.all_gather(gathered, mine_t)
+        per_rank = [[float(v) for v in g.cpu()] for g in gathered]
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0]), float(t[1])
@@ -408,6 +416,13 @@ def main():
                                    (" (--force-dist: the N > 1 step at world size %d)" % world
                                     if args.force_dist else "")},
             "samples_per_step": npix_total * spp,
+            **({"ranks": {"kernel_ms_per_launch": [round(r[1], 2) for r in per_rank],
+                          "step_ms": [round(r[0] / args.steps * 1e3, 1) for r in per_rank],
+                          "pixels": [int(r[2]) for r in per_rank],
+                          "queries": [int(r[3]) for r in per_rank],
+                          "kernel_imbalance_max_over_mean": round(
+                              max(r[1] for r in per_rank) / max(1e-9, sum(r[1] for r in per_rank) / world), 4)}}
+               if per_rank and world > 1 else {}),
             "queries_per_sample": round(queries / samples, 2),
         }
         opq = OPS_PER_QUERY.get(cfg.name)
@@ -436,7 +451,11 @@ def main():
                     "salu_insts_per_simd_cycle": round(ev.get("salu_insts_per_simd_cycle", 0), 4),
                     "valu_busy_rocprof": round(ev["valu_busy"], 4),
                     "hbm_GBps": round(ev["hbm_GBps"], 2), "hbm_peak_GBps": 8000.0})
-        if not args.no_cpu:  # rank 0, after the timed region (the other ranks are done)
+        if world > 1 and not args.no_cpu and not args.cpu_at_n:
+            # the CPU baseline is the N = 1 line's (rank 0 at N = 1 only); an N-rank frame is the
+            # one-GPU frame bit for bit (tiles) or within ~1e-7 (sample split), tests/test_bench_dist.py
+            out["cpu_baseline"] = {"note": "reported on the N = 1 line (bench.py --gpus 1); --cpu-at-n adds it here"}
+        elif not args.no_cpu:  # rank 0, after the timed region (the other ranks are done)
             try:
                 npx = args.cpu_pixels or CPU_PIXELS.get(cfg.name, 512)
                 pix, ref, cb = cpu_baseline(cfg, to_text(root, "/tmp/pt_bench_img"), spp, npx,

@@ -46,11 +46,15 @@ def test_bench_two_ranks_gloo(tmp_path, split):
     # block-staged path (whole 32-sample blocks) a real rank share takes
     common = ["--config", "C3", "--spp", "256", "--steps", "1", "--warmup", "0", "--cpu-pixels", "16"]
     one, f1 = _bench(common + ["--no-cpu"], 1, tmp_path, "one")
-    two, f2 = _bench(common + ["--backend", "gloo", "--split", split], 2, tmp_path, "two")
+    two, f2 = _bench(common + ["--backend", "gloo", "--split", split, "--cpu-at-n"], 2, tmp_path, "two")
     assert two["n_gpus"] == 2 and two["steps"] == 1
     assert "gloo reduce" in two["config"]["sharding"]
     assert ("spp split" in two["config"]["sharding"]) == (split == "samples")
     assert two["samples_per_step"] == one["samples_per_step"] == 1920 * 1080 * 256
+    rk = two["ranks"]  # each rank's own numbers, as the driver's N-GPU line carries them
+    assert len(rk["kernel_ms_per_launch"]) == 2 and rk["kernel_imbalance_max_over_mean"] >= 1.0
+    assert sum(rk["pixels"]) == (1920 * 1080 * (2 if split == "samples" else 1))
+    assert sum(rk["queries"]) == pytest.approx(two["queries_per_sample"] * two["samples_per_step"], rel=1e-4)
     # the same frame: the same span queries in total, split over the ranks
     assert two["queries_per_sample"] == pytest.approx(one["queries_per_sample"], rel=1e-9)
     # roofline: each rank's launches carry half the work; the kernel time is the max over ranks
