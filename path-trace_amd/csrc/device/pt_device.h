@@ -1420,6 +1420,116 @@ struct Diff
 /* TransformedObject (include/object.h:26-76): the child sees the ray mapped by
  * m; span normals are mapped back by normalize(inv.applyNoTranslate(n)).
  * P[MOFF..+12] = m, P[IOFF..+12] = inverse(m) (transform.h:350-383, host). */
+/* ---- union-only passes with the sphere roots compacted per lane ----------
+ * (PT_SPH_COMPACT) A fast pass over a tree of Unions, spheres and planes takes
+ * the union rule (union_first_hit) as an accumulation whose result does not
+ * depend on the order the spans arrive in (the minimum start, a tie on it,
+ * a NaN anywhere).  So the spheres' roots and quotients need not run sphere
+ * by sphere on the whole wave whenever one lane meets the sphere: each lane
+ * first marks the spheres it meets (the discriminant alone), then every lane
+ * walks its own marked spheres, reading their contexts from an LDS table by
+ * primitive index -- the wave loops as many times as its lanes' largest
+ * count, not once per sphere any lane meets. */
+#ifndef PT_SPH_COMPACT
+#define PT_SPH_COMPACT 1
+#endif
+struct UnionAcc
+{
+    int found = 0, tie = 0, bad = 0, bm = 0;
+    float b0 = 0.0f;
+    __device__ __forceinline__ void add(int live, float t0, float t1, int m)
+    {
+        const int cand = live & (t1 >= EPS);
+        const int better = cand & ((!found) | (t0 < b0));
+        tie = better ? 0 : (tie | (cand & (t0 == b0)));
+        bad |= live & ((t0 != t0) | (t1 != t1));
+        b0 = better ? t0 : b0;
+        bm = better ? m : bm;
+        found |= cand;
+    }
+};
+template <class N>
+struct Compact
+{
+    static constexpr bool OK = false;
+};
+template <int P, int O, int M>
+struct Compact<Sph<P, O, M>>
+{
+    static constexpr bool OK = P < 64;
+    __device__ static __forceinline__ void run(UnionAcc &, u64 &m, const typename Sph<P, O, M>::Ctx &c, const Ray &q,
+                                               const Env &)
+    {
+        const float b = dot(c.omc, q.d);
+        const float disc = b * b - q.a * c.c;
+        if (!(disc <= EPS))
+            m |= 1ull << P;
+    }
+    __device__ static __forceinline__ void fill(float4 *tab, int *mt, const typename Sph<P, O, M>::Ctx &c)
+    {
+        tab[P] = make_float4(c.omc.x, c.omc.y, c.omc.z, c.c);
+        mt[P] = M;
+    }
+};
+template <int P, int O, int M, int AX, int U>
+struct Compact<Pln<P, O, M, AX, U>>
+{
+    static constexpr bool OK = true;
+    __device__ static __forceinline__ void run(UnionAcc &acc, u64 &, const typename Pln<P, O, M, AX, U>::Ctx &c,
+                                               const Ray &q, const Env &e)
+    {
+        typename Pln<P, O, M, AX, U>::St s;
+        Pln<P, O, M, AX, U>::init(s, c, q, e);
+        acc.add(s.live, s.t0, s.t1, M);
+    }
+    __device__ static __forceinline__ void fill(float4 *, int *, const typename Pln<P, O, M, AX, U>::Ctx &) {}
+};
+template <class A, class B>
+struct Compact<Uni<A, B>>
+{
+    static constexpr bool OK = Compact<A>::OK && Compact<B>::OK;
+    __device__ static __forceinline__ void run(UnionAcc &acc, u64 &m, const typename Uni<A, B>::Ctx &c, const Ray &q,
+                                               const Env &e)
+    {
+        Compact<A>::run(acc, m, c.a, q, e);
+        Compact<B>::run(acc, m, c.b, q, e);
+    }
+    __device__ static __forceinline__ void fill(float4 *tab, int *mt, const typename Uni<A, B>::Ctx &c)
+    {
+        Compact<A>::fill(tab, mt, c.a);
+        Compact<B>::fill(tab, mt, c.b);
+    }
+};
+/* union_first_hit's result for a Compact tree: planes in line, the marked
+ * spheres walked per lane from the table */
+template <class R>
+__device__ __forceinline__ int compact_first_hit(const typename R::Ctx &ctx, const Ray &q, const Env &e,
+                                                 const float4 *tab, const int *mt, bool &hit, float &t, int &mat)
+{
+    UnionAcc acc;
+    u64 m = 0ull;
+    Compact<R>::run(acc, m, ctx, q, e);
+    while (wave_any(m != 0ull)) {
+        if (m != 0ull) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const float4 sp = tab[k];
+            const float b = (sp.x * q.d.x + sp.y * q.d.y) + sp.z * q.d.z; /* dot(omc, d), Sph::init */
+            const float disc = b * b - q.a * sp.w;
+            const float sq = sqrt_core(disc); /* exact: disc > EPS (or inf / NaN) on a marked sphere */
+            const float n0 = -b - sq, n1 = -b + sq;
+            float t0 = div_core(n0, q.ra), t1 = div_core(n1, q.ra);
+            if (!(q.aok && num_ok(n0) && num_ok(n1)))
+                t0 = n0 / q.a, t1 = n1 / q.a;
+            acc.add(1, t0, t1, mt[k]);
+        }
+    }
+    mat = acc.bm;
+    t = acc.b0;
+    hit = acc.found && acc.b0 < MAXV;
+    return ((!acc.found) | ((acc.b0 >= EPS) & !acc.tie)) & !acc.bad;
+}
+
 template <int MOFF, int IOFF, class C>
 struct Xf
 {
@@ -2415,6 +2525,8 @@ struct WaveLds
     unsigned char *slowq; /* PT_SCAP slots waiting for the full merge (ring number mod 256) */
     unsigned char *midq;  /* PT_SCAP slots the clear pass could not finish (fast check next) */
     float *lsum;          /* the fast order's 64 lane sums, x / y / z planes (lsum_lds scenes) */
+    float4 *stab;         /* PT_SPH_COMPACT: the burst origin's sphere contexts by primitive index */
+    int *smat;            /* ... and their materials */
 };
 
 /* ---------------------------------------------------------------- spine --- */
@@ -2715,6 +2827,8 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     typename S::Root::Ctx c0;
     S::Root::prep(c0, hit, e);
     lds_put(*cxp, c0);
+    if constexpr (PT_SPH_COMPACT && Compact<typename S::Root>::OK)
+        Compact<typename S::Root>::fill(L.stab, L.smat, c0);
     /* The burst's leaf children form one run of the fast order (oracle.cpp
      * ORDER_FAST): the run's non-zero terms are dealt round-robin to 64 lane
      * sums (lsum; the k-th one to lane k mod 64), which are added into retval
@@ -3148,11 +3262,28 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
 #else
             const typename S::Root::Ctx ctx = lds_get(*cxp);
 #endif
+            int fok;
+#if PT_UNION_FUSED && !PT_PASS_PAIR_FALLBACK
+            if constexpr (PT_SPH_COMPACT && Compact<typename S::Root>::OK) {
+                bool fh;
+                float t;
+                int mat;
+                fok = compact_first_hit<typename S::Root>(ctx, mkray_unit(dir), e, L.stab, L.smat, fh, t, mat);
+                if (fok) {
+                    V3 col = mk(0, 0, 0);
+                    if (fh)
+                        col = S::emis(mat, hit + t * dir, e);
+                    const V3 term = ((aN * en.w) * rc) * col;
+                    ring[pos & (PT_RCAP - 1)] = make_float4(term.x, term.y, term.z, 0.0f);
+                    return true;
+                }
+                return false;
+            }
+#endif
             PrimSpans<S::Root::HI> ps;
             PT_MARK(9);
             S::Root::span(ps, ctx, mkray_unit(dir), e);
             PT_MARK(10);
-            int fok;
 #if PT_UNION_FUSED && !PT_PASS_PAIR_FALLBACK
             if constexpr (S::Root::UNION_ONLY) {
                 bool fh;
@@ -4260,6 +4391,9 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     __shared__ Counters cbuf[PT_WPW];
     constexpr bool LSUM_LDS = lsum_lds<S, MAXD>();
     __shared__ float lsbuf[PT_WPW][LSUM_LDS ? 3 * 64 : 1];
+    constexpr bool SCOMPACT = PT_SPH_COMPACT && Compact<typename S::Root>::OK;
+    __shared__ float4 stbuf[PT_WPW][SCOMPACT ? S::Root::HI : 1];
+    __shared__ int smbuf[PT_WPW][SCOMPACT ? S::Root::HI : 1];
     /* a chunk's lanes while the wave walks its samples one by one: (pixel,
      * sample | hit << 30 | exit << 31, camera t, camera ref), replaced by the
      * sample's result (x, y, z) once it is traced; in LDS rather than in
@@ -4308,7 +4442,8 @@ __device__ __forceinline__ void render_chunk(const float *__restrict__ P, const 
     cnt.sp[0] = cnt.sp[1] = cnt.sp[2] = 0;
     cnt.ch[0] = cnt.ch[1] = cnt.ch[2] = 0;
 #endif
-    const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave], LSUM_LDS ? lsbuf[wave] : nullptr};
+    const WaveLds L = {&xbuf[wave], rbuf[wave], sbuf[wave], mbuf[wave], LSUM_LDS ? lsbuf[wave] : nullptr,
+                       stbuf[wave], smbuf[wave]};
     const int CH = lp.chunk > 0 ? lp.chunk : PT_CHUNK; /* small launches use smaller chunks */
     const long long n_chunks = (lp.n_items + CH - 1) / CH;
     /* Split launches (lane-walk scenes, see pt_render_light): the full kernel
