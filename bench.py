@@ -166,7 +166,8 @@ def launch_check(args):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd, env=env)
+    rc = subprocess.call(cmd, env=env)
+    return rc if rc >= 0 else 128 - rc  # a rank launcher killed by a signal: the shell's 128 + signal
 
 
 def _atoi(text: str) -> int:
