@@ -1086,9 +1086,16 @@ private:
             cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
             if (queue_.empty() && stop_)
                 return;
-            cv_.wait_for(lk, std::chrono::microseconds(maxWaitUs_),
-                         [&] { return stop_ || queue_.size() >= maxBatch_; });
+            /* a batch launches at maxBatch, after maxWaitUs -- or as soon as
+             * as many calls wait as the previous batch held: the steady state
+             * of N threads each asking for one pixel at a time, which then
+             * costs no batching window at all (a thread that stops calling
+             * costs one window, after which the size adapts) */
+            cv_.wait_for(lk, std::chrono::microseconds(maxWaitUs_), [&] {
+                return stop_ || queue_.size() >= maxBatch_ || (lastBatch_ > 0 && queue_.size() >= lastBatch_);
+            });
             const size_t n = std::min(queue_.size(), maxBatch_);
+            lastBatch_ = n;
             std::vector<Req *> batch(queue_.begin(), queue_.begin() + (std::ptrdiff_t)n);
             queue_.erase(queue_.begin(), queue_.begin() + (std::ptrdiff_t)n);
             lk.unlock();
@@ -1117,6 +1124,7 @@ private:
     mutable std::mutex m_;
     std::condition_variable cv_, done_;
     std::vector<Req *> queue_;
+    size_t lastBatch_ = 0;
     bool stop_ = false;
     uint64_t launches_ = 0, pixels_ = 0;
     std::thread worker_; /* last: started once every member above is constructed */
