@@ -198,6 +198,17 @@ typedef struct pt_render_stats {
  * events and the counter read-back (the per-pixel caller's fast path). */
 int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_stats *stats);
 
+/* The multi-GPU partition (replaces the reference's TCP block farm,
+ * src/test.cpp:520-778): the pixel indices (y * width + x, raster order) rank
+ * `rank` of `world` renders in the lattice deal of tile x tile tiles -- tile
+ * (tx, ty) belongs to rank (tx + 3 ty) mod world -- the default of bench.py
+ * and pathtrace.dist.rank_pixels.  Every pixel has exactly one owner, so the
+ * ranks' frames (pt_render_device with the list into a zeroed full frame)
+ * sum to the one-GPU frame bit for bit.  pixels = NULL: *count receives the
+ * number only; else at most capacity indices are written. */
+int pt_rank_pixels(int width, int height, int rank, int world, int tile, int32_t *pixels, int64_t capacity,
+                   int64_t *count);
+
 /* Host-clock phases (microseconds) of the calling thread's last pt_render --
  * the breakdown of a per-pixel tracePixel call.  out[k]
  * for k < n: */

@@ -1653,6 +1653,33 @@ int pt_render(pt_scene *s, const pt_render_params *p, float *rgb_out, pt_render_
     });
 }
 
+int pt_rank_pixels(int width, int height, int rank, int world, int tile, int32_t *pixels, int64_t capacity,
+                   int64_t *count)
+{
+    return guard([&] {
+        if (width <= 0 || height <= 0 || (int64_t)width * height >= (1ll << 31))
+            throw Error(PT_ERR_ARG, "bad frame size");
+        if (world < 1 || rank < 0 || rank >= world || tile < 1)
+            throw Error(PT_ERR_ARG, "need 0 <= rank < world and tile >= 1");
+        if (!count || (pixels && capacity < 0))
+            throw Error(PT_ERR_ARG, "null count or negative capacity");
+        int64_t n = 0;
+        for (int y = 0; y < height; y++)
+            for (int x = 0; x < width; x++) {
+                const int64_t owner = world == 1 ? 0 : ((int64_t)(x / tile) + 3ll * (y / tile)) % world;
+                if (owner != rank)
+                    continue;
+                if (pixels && n < capacity)
+                    pixels[n] = y * width + x;
+                n++;
+            }
+        *count = n;
+        if (pixels && n > capacity)
+            throw Error(PT_ERR_ARG, "capacity below the rank's pixel count");
+        return PT_OK;
+    });
+}
+
 int pt_call_profile(double *out, int n)
 {
     if (!out || n < 0)

@@ -99,6 +99,7 @@ SIGNATURES = {
     "pt_render_device_timed": (_I, [_P, ctypes.POINTER(RenderParams), _P, _P]),
     "pt_render_collect": (_I, [_P, _I, ctypes.POINTER(RenderStats)]),
     "pt_call_profile": (_I, [ctypes.POINTER(ctypes.c_double), _I]),
+    "pt_rank_pixels": (_I, [_I, _I, _I, _I, _I, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
     "pt_render_adaptive": (_I, [_P, ctypes.POINTER(RenderParams), ctypes.POINTER(AdaptiveParams), _P,
                                 ctypes.POINTER(RenderStats)]),
     "pt_trace_rays": (_I, [_P, ctypes.POINTER(TraceParams), _P, ctypes.c_int64, _P, ctypes.POINTER(RenderStats)]),

@@ -131,3 +131,17 @@ def test_lattice_balances_a_clustered_cost_map():
 
     lat, hashed = imbalance("lattice", 4), imbalance("hashed", 16)
     assert lat < 1.01 and lat < hashed, (lat, hashed)
+
+
+@pytest.mark.parametrize("W,H,world,tile", [(1920, 1080, 8, 4), (100, 37, 3, 4), (64, 40, 2, 1), (33, 17, 5, 8)])
+def test_c_abi_partition_equals_python(built, W, H, world, tile):
+    """pt_rank_pixels (the C hosts' partition) is pathtrace.dist.rank_pixels' lattice deal"""
+    import ctypes
+    from pathtrace import _lib
+    L = _lib.lib()
+    for r in range(world):
+        n = ctypes.c_int64(0)
+        _lib.check(L.pt_rank_pixels(W, H, r, world, tile, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(1, n.value), np.int32)
+        _lib.check(L.pt_rank_pixels(W, H, r, world, tile, out.ctypes.data, n.value, ctypes.byref(n)))
+        np.testing.assert_array_equal(out[:n.value], ptdist.rank_pixels(W, H, r, world, tile=tile))

@@ -572,3 +572,16 @@ def test_block_staged_pixel_sums(built, tmp_path):
     per = O.render(txt, W, H, spp, depth, pixels=pix, order=O.ORDER_FAST, per_sample=True)
     assert_bits(block_sum(per) / np.float32(spp), o, "numpy block sums vs oracle")
     assert_bits(one.reshape(-1, 3)[pix], o, "block-staged vs oracle")
+
+
+@pytest.mark.gpu
+def test_pixel_list_duplicates_and_order(built):
+    """A pixel list in any order, with repeats (a caller's blocks overlapping
+    at their corners, src/test.cpp:466-499): every entry gets its pixel's
+    frame value bit for bit -- the engine is keyed by the pixel, not the slot."""
+    W, H, spp, depth = 40, 24, 4, 8
+    ds = pt.DeviceScene(scenes.scene_p1())
+    frame = pt.render(ds, W, H, spp, depth).reshape(-1, 3)
+    pix = np.array([5, 939, 5, 0, 477, 939, 939, 12, W * H - 1, 0], np.int32)
+    got = pt.render(ds, W, H, spp, depth, pixels=pix)
+    np.testing.assert_array_equal(got.view(np.uint32), frame[pix].view(np.uint32))
