@@ -15,6 +15,7 @@
 #include <sstream>
 #include <vector>
 
+#include <cfloat>
 #include <cmath>
 #include "internal.h"
 
@@ -41,6 +42,55 @@ struct Gen
     std::vector<int> user_obj;   /* User objects reached (their bodies become UObjB_<id>) */
 
     explicit Gen(const SceneImpl &sc) : s(sc) {}
+
+    /* A bound on |getColor| of texture id over every input point, as the
+     * device evaluates it (pt_device.h T* templates), or +inf when none is
+     * known (NaN, infinities, user code, TCoord).  Image lookups are
+     * bounds-checked (a miss is +0), so an image texture is bounded by its
+     * texels whatever point it is asked about; the maps and transforms only
+     * move the point; LogTexture's filter lies in (0.1, 1] for finite input. */
+    double color_bound(int id, int guard = 0) const
+    {
+        const double INF = HUGE_VAL;
+        if (guard > 64)
+            return INF;
+        const TexRec &x = s.textures.at(id);
+        auto fin = [](double v) { return std::fabs(v) <= (double)FLT_MAX ? std::fabs(v) : HUGE_VAL; };
+        auto img = [&](int k) {
+            if (k < 0 || k >= (int)s.images.size())
+                return 0.0;
+            double b = 0.0;
+            for (float v : s.images[k].rgba) b = std::max(b, fin(v));
+            return b;
+        };
+        double b = 0.0;
+        switch (x.kind) {
+        case TexKind::Color:
+            for (int c = 0; c < 3; c++) b = std::max(b, fin(x.f[c]));
+            return b;
+        case TexKind::Image:
+        case TexKind::ImageAlpha:
+            return img(x.img[0]);
+        case TexKind::Skybox:
+        case TexKind::SkyboxAlpha:
+            for (int k = 0; k < 6; k++) b = std::max(b, img(x.img[k]));
+            return b;
+        case TexKind::Multiply:
+            for (int c = 0; c < 3; c++) b = std::max(b, fin(x.f[c]));
+            b *= color_bound(x.child, guard + 1);
+            return b <= (double)FLT_MAX ? b : INF; /* a product of finite floats below FLT_MAX rounds finite */
+        case TexKind::Log:
+            return color_bound(x.child, guard + 1) <= (double)FLT_MAX ? 1.0 : INF;
+        case TexKind::MirrorBall:
+        case TexKind::Spherical:
+        case TexKind::Xform:
+            return color_bound(x.child, guard + 1);
+        case TexKind::Coord:
+        case TexKind::User:
+            return INF;
+        }
+        return INF;
+    }
 
     int put(const float *v, int n)
     {
@@ -413,6 +463,12 @@ Generated generate(const SceneImpl &s, int depth, bool rays)
         src << "m == " << k << " ? " << (z ? "true" : "false") << " : ";
     }
     src << "false; }\n";
+    /* emis_finite: every material's emission is finite wherever it is looked
+     * up, so a child of weight +-0 adds +-0 (pt_device.h zero_child) */
+    bool emis_finite = true;
+    for (size_t k = 0; k < g.mats.size() && emis_finite; k++)
+        emis_finite = g.color_bound(s.materials.at(g.mats[k]).emissive) <= (double)FLT_MAX;
+    src << "  static constexpr bool emis_finite = " << (emis_finite ? "true" : "false") << ";\n";
     if (all_emis_const && lit_mats.size() <= 4) {
         /* few constant emitters: a select chain on scalar-loaded constants
          * (dark materials keep the exact (+0, +0, +0)) instead of a per-lane

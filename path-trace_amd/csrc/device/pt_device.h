@@ -3593,6 +3593,26 @@ enum { RS_REFRACT, RS_SCATTER };
 
 /* One sample = one traceRay tree (path-trace.h:58-165) + the jittered camera
  * ray of tracePixel (path-trace.h:190-198).  F = this wave's frame stack. */
+/* A child of weight +-0 whose query need not run (PT_ZERO_CHILD).  The
+ * reference folds a finished child as retval += w * r (path-trace.h:118,
+ * :162).  A mirror child off a surface with reflectance 0 -- a sky or
+ * emitter hit, which has no scatter loop -- has w = ((add / N) factor) rc =
+ * +-0 and strength ... |rc| = 0 < eps, so its traceRay returns at once with
+ * r = the emission where it lands, or 0 on a miss (path-trace.h:97-108).  When
+ * every emission is finite (Scene::emis_finite: constant and image texels
+ * bounded, codegen color_bound), w * r is +-0, and part + +-0 == part exactly
+ * unless part is -0 or NaN -- checked here.  The skipped query still counts
+ * as a query in the statistics. */
+#ifndef PT_ZERO_CHILD
+#define PT_ZERO_CHILD 1
+#endif
+__device__ __forceinline__ bool zero_child(V3 w, float cstr, int cdep, V3 part)
+{
+    const u32 wz = (__float_as_uint(w.x) | __float_as_uint(w.y) | __float_as_uint(w.z)) << 1;
+    auto ok = [](float v) { return v == v && __float_as_uint(v) != 0x80000000u; };
+    return wz == 0u && (cdep <= 0 || cstr < EPS) && ok(part.x) && ok(part.y) && ok(part.z);
+}
+
 /* The camera query of a sample, found ahead of time by one lane of the wave
  * (render_chunk traces a chunk's camera rays one per lane). */
 struct CamHit
@@ -3664,6 +3684,13 @@ __device__ __forceinline__ bool lane_sample(const Env &e, int depth, V3 o, V3 d,
     if (!(depth - 1 <= 0 || cs < EPS))
         return false;
     nq = 2;
+#if PT_ZERO_CHILD
+    if constexpr (S::emis_finite)
+        if (zero_child(w, cs, depth - 1, retval)) {
+            res = (z + retval) / 1.0f;
+            return true;
+        }
+#endif
     typename S::Root::Ctx ctx;
     S::Root::prep_l(ctx, hit, e);
     float t2 = 0.0f;
@@ -3808,6 +3835,18 @@ __device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 o0, V3 d0
                 w.md = refl;
                 w.ms = (((str / 1.0f) * add) * factor) * length(rc);
             }
+            /* a mirror child of weight +-0 (zero_child): without a refraction
+             * child it is skipped here, with one once that child's sum is
+             * known (mode 3) */
+            bool zM = false;
+#if PT_ZERO_CHILD
+            if constexpr (S::emis_finite)
+                zM = hasM && zero_child(w.wM, w.ms, w.mdep, hasR ? mk(0, 0, 0) : retval);
+#endif
+            if (zM && !hasR) {
+                nq++;
+                hasM = false;
+            }
             if (!hasR && !hasM) {
                 r = retval;
                 descend = false;
@@ -3817,7 +3856,7 @@ __device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 o0, V3 d0
                 ok = false;
                 continue;
             }
-            w.mode = hasR ? (hasM ? 0 : 1) : 2;
+            w.mode = hasR ? (hasM ? (zM ? 3 : 0) : 1) : 2;
             push(w);
             if (hasR)
                 o = hit, d = rd, str = sR, dep = dep - 1;
@@ -3829,8 +3868,14 @@ __device__ __forceinline__ bool lane_walk(const Env &e, int depth0, V3 o0, V3 d0
                 done = true;
                 continue;
             }
-            if (F[0].mode == 0) {
+            if (F[0].mode == 0 || F[0].mode == 3) {
                 F[0].part = F[0].part + F[0].wR * r;
+                if (F[0].mode == 3 && zero_child(F[0].wM, F[0].ms, F[0].mdep, F[0].part)) {
+                    nq++; /* the mirror child's query, skipped */
+                    r = F[0].part;
+                    pop();
+                    continue;
+                }
                 F[0].mode = 2;
                 o = F[0].mo, d = F[0].md, str = F[0].ms, dep = F[0].mdep;
                 descend = true;
@@ -4258,11 +4303,21 @@ __device__ __forceinline__ V3 trace_sample(const Env &e, const PtLaunch &lp, int
                 const V3 refl = univ(f.refl), n = univ(f.n), rc = univ(f.rc);
                 const float sc = unif(f.sc), add = unif(f.add), N = (float)uni(f.N);
                 float factor = 1.0f - (1.0f - dot(refl, n)) * sc;
-                f.w = ((add / N) * factor) * rc;
+                const V3 w = ((add / N) * factor) * rc;
+                const float cstr = (((unif(f.strength) / N) * add) * factor) * length(rc);
+#if PT_ZERO_CHILD
+                if constexpr (S::emis_finite)
+                    if (zero_child(w, cstr, uni(f.depth) - 1, univ(f.retval))) {
+                        cnt.queries++; /* the child's query, skipped */
+                        f.i = uni(f.i) + 1;
+                        continue;
+                    }
+#endif
+                f.w = w;
                 f.resume = RS_SCATTER;
                 Frame &c = F[sp + 1];
                 c.o = univ(f.hit), c.d = refl;
-                c.strength = (((unif(f.strength) / N) * add) * factor) * length(rc);
+                c.strength = cstr;
                 c.depth = uni(f.depth) - 1;
                 sp++;
                 phase = PH_ENTER;

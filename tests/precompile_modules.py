@@ -39,6 +39,9 @@ def test_jobs():
     from test_user_object import p0, box_scene
     jobs += [((lambda: pt.DeviceScene(p0(True))), 6), ((lambda: pt.DeviceScene(p0(False))), 6),
              ((lambda: pt.DeviceScene(box_scene())), 6), ((lambda: pt.DeviceScene(box_scene()).compile_queries()), None)]
+    # tests/test_zero_child.py: skies of finite and non-finite emission
+    from test_zero_child import CASES as ZC_CASES, SKIES, sky_scene, DEPTH as ZC_DEPTH
+    jobs += [((lambda s=s, k=k: pt.DeviceScene(sky_scene(SKIES[s]()), lane_walk=k)), ZC_DEPTH) for (s, k) in ZC_CASES]
     return jobs
 
 
