@@ -1530,6 +1530,90 @@ __device__ __forceinline__ int compact_first_hit(const typename R::Ctx &ctx, con
     return ((!acc.found) | ((acc.b0 >= EPS) & !acc.tie)) & !acc.bad;
 }
 
+/* ---- leaf children occluded by a plane (PT_OCCLUDE) ----------------------
+ * In a tree of Unions, spheres and planes the first hit of a ray is the
+ * earliest merged span (src/union.cpp:84-134): its start material when the
+ * start reaches eps, else nothing when it runs to max_value
+ * (path-trace.h:66-96).  A non-emissive plane whose solid the child ray
+ * enters at t_P (origin outside, d.n < 0) gives the span [t_P, max_value],
+ * so the merged span holding it, and every span before it, starts at or
+ * before t_P.  If every emissive primitive's span starts after t_P, the hit
+ * is non-emissive or none: the child's term is weight * (+0, +0, +0), zero
+ * for the finite weights RAW already requires, like a dark child's.
+ * T_E, a lower bound on the emissive starts from the burst origin, is taken
+ * once per burst: an emissive plane the origin is outside of (num <= -1e-3)
+ * cannot be met before |num| / |n| (less 0.1 % for the rounding of the
+ * computed quotient); an emissive sphere, or an origin inside an emissive
+ * plane's solid, gives T_E = 0 (no claim).  Per attempt, on the
+ * unnormalised w with |w| <= B = (1 + |kR|) 1.0001 (accepted: |v| < 1), an
+ * axis-aligned occluder (the exact n.w = n_a w_a) is entered before T_E when
+ * n_a w_a < -|num_P| B 1.001 / T_E: the normalised direction's quotient is
+ * then at most T_E (1 + 3e-6) / 1.001.  The occluder needs |n_a w_a| > 1e-4
+ * (a non-degenerate span) and num_P <= -1e-3. */
+#ifndef PT_OCCLUDE
+#define PT_OCCLUDE 1
+#endif
+template <class N>
+struct Occl
+{
+    static constexpr bool OK = false;
+};
+template <int P, int O, int M>
+struct Occl<Sph<P, O, M>>
+{
+    static constexpr bool OK = true;
+    template <class SEL>
+    __device__ static __forceinline__ float emis_lb(const typename Sph<P, O, M>::Ctx &, const Env &)
+    {
+        return SEL::take(M) ? 0.0f : __builtin_inff();
+    }
+    template <class SEL>
+    __device__ static __forceinline__ u64 occ(const typename Sph<P, O, M>::Ctx &, V3, float, const Env &)
+    {
+        return 0ull;
+    }
+};
+template <int P, int O, int M, int AX, int U>
+struct Occl<Pln<P, O, M, AX, U>>
+{
+    static constexpr bool OK = true;
+    template <class SEL>
+    __device__ static __forceinline__ float emis_lb(const typename Pln<P, O, M, AX, U>::Ctx &c, const Env &e)
+    {
+        if constexpr (!SEL::take(M))
+            return __builtin_inff();
+        const float nn = __builtin_sqrtf(dot(mk(e.P[O], e.P[O + 1], e.P[O + 2]), mk(e.P[O], e.P[O + 1], e.P[O + 2])));
+        return c.num <= -1e-3f ? (-c.num / nn) * 0.999f : 0.0f;
+    }
+    template <class SEL>
+    __device__ static __forceinline__ u64 occ(const typename Pln<P, O, M, AX, U>::Ctx &c, V3 w, float g, const Env &e)
+    {
+        if constexpr (SEL::take(M) || AX < 0) {
+            return 0ull;
+        } else {
+            const float na = e.P[O + (AX >> 1)];
+            const float wa = (AX >> 1) == 0 ? w.x : (AX >> 1) == 1 ? w.y : w.z;
+            const float lim = fmaxf(1e-4f, -c.num * g);
+            return __ballot(c.num <= -1e-3f && na * wa < -lim);
+        }
+    }
+};
+template <class A, class B>
+struct Occl<Uni<A, B>>
+{
+    static constexpr bool OK = Occl<A>::OK && Occl<B>::OK;
+    template <class SEL>
+    __device__ static __forceinline__ float emis_lb(const typename Uni<A, B>::Ctx &c, const Env &e)
+    {
+        return fminf(Occl<A>::template emis_lb<SEL>(c.a, e), Occl<B>::template emis_lb<SEL>(c.b, e));
+    }
+    template <class SEL>
+    __device__ static __forceinline__ u64 occ(const typename Uni<A, B>::Ctx &c, V3 w, float g, const Env &e)
+    {
+        return Occl<A>::template occ<SEL>(c.a, w, g, e) | Occl<B>::template occ<SEL>(c.b, w, g, e);
+    }
+};
+
 template <int MOFF, int IOFF, class C>
 struct Xf
 {
@@ -2868,6 +2952,25 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
     const bool wfin = __builtin_fabsf(rc.x) < 1e37f && __builtin_fabsf(rc.y) < 1e37f && __builtin_fabsf(rc.z) < 1e37f;
     const u64 raw_mask =
         uni_mask((KR0 || length(kR) < 64.0f) && wfin && S::Root::template dark_pre<Emissive<S>>(c0, e));
+    /* children that enter a non-emissive plane before any emissive
+     * primitive can be met are dark too (Occl, PT_OCCLUDE): occ_g = B 1.001 / T_E */
+#if PT_OCCLUDE
+    constexpr bool OCC = RAW && Occl<typename S::Root>::OK;
+#else
+    constexpr bool OCC = false;
+#endif
+    float occ_g = __builtin_inff();
+    if constexpr (OCC) {
+        const float te = fminf(Occl<typename S::Root>::template emis_lb<Emissive<S>>(c0, e), 1e19f);
+        const float bw = (KR0 ? 1.0f : 1.0f + length(kR)) * 1.0001f;
+        occ_g = unif(te > 0.0f ? bw * 1.001f / te : __builtin_inff());
+    }
+    auto dark = [&](V3 wn) -> u64 {
+        u64 d = S::Root::template dark_mask<Emissive<S>>(c0, wn, e);
+        if constexpr (OCC)
+            d |= Occl<typename S::Root>::template occ<Emissive<S>>(c0, wn, occ_g, e);
+        return d & raw_mask;
+    };
     /* children recurse for factor >= eps / (sNa |rc|): short rounds when that
      * is below 0.99 (over 1 % of the children recurse) */
     const bool short_nd = !DEFERRED && EPS < 0.99f * (sNa * abs_rc);
@@ -2961,7 +3064,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
                         u64 D = 0ull;
                         if (RAW)
-                            D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
+                            D = dark(wn);
                         abits = shl_lane_bit(abits, ap.A[h]);
                         fbits = shl_lane_bit(fbits, ap.F[h]);
                         kbits = shl_lane_bit(kbits, ap.A[h] & ~D);
@@ -3036,7 +3139,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
                         u64 D = 0ull;
                         if (RAW)
-                            D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
+                            D = dark(wn);
                         K[kk] = ap.A[h] & ~D;
                         ta += __popcll(ap.A[h]);
                         tk += __popcll(K[kk]);
@@ -3060,7 +3163,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
                         u64 D = 0ull;
                         if (RAW)
-                            D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
+                            D = dark(wn);
                         K[k + h] = ap.A[h] & ~D;
                         ta += __popcll(ap.A[h]);
                         tk += __popcll(K[k + h]);
@@ -3116,7 +3219,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         const V3 wn = h ? mk(ap.x.y, ap.y.y, ap.z.y) : mk(ap.x.x, ap.y.x, ap.z.x);
                         u64 D = 0ull;
                         if (RAW)
-                            D = S::Root::template dark_mask<Emissive<S>>(c0, wn, e) & raw_mask;
+                            D = dark(wn);
                         write_attempt(ap.A[h], ap.A[h] & ~D, h ? sk1 : sk, wn, 0.0f);
                         if (k + h == katt - 1)
                             Alast = ap.A[h], Flast = ap.F[h];
@@ -3177,7 +3280,7 @@ __device__ __forceinline__ int burst_t(const Env &e, Rng &rng, const u64 *__rest
                         at[k] = attempt<DEFERRED, KR0>(sk, n, kR, sc, sNa, abs_rc, child_leaf_depth);
                         Dm[k] = 0ull;
                         if (RAW)
-                            Dm[k] = S::Root::template dark_mask<Emissive<S>>(c0, at[k].wn, e) & raw_mask;
+                            Dm[k] = dark(at[k].wn);
                     }
                 }
                 m = 0;
