@@ -42,6 +42,9 @@ def test_jobs():
     # tests/test_zero_child.py: skies of finite and non-finite emission
     from test_zero_child import CASES as ZC_CASES, SKIES, sky_scene, DEPTH as ZC_DEPTH
     jobs += [((lambda s=s, k=k: pt.DeviceScene(sky_scene(SKIES[s]()), lane_walk=k)), ZC_DEPTH) for (s, k) in ZC_CASES]
+    # tests/test_occlude.py: plane occluders near the emitters
+    from test_occlude import VARIANTS as OC_VARIANTS, DEPTH as OC_DEPTH
+    jobs += [((lambda v=v: pt.DeviceScene(zoo.occlude_box(v))), OC_DEPTH) for v in OC_VARIANTS]
     return jobs
 
 
@@ -75,4 +78,6 @@ TEST_DEFINES = [("PT_ROOM_CAP=3", "scene_p1", 8, False), ("PT_ROOM_CAP=40", "sce
                 ("PT_LANE_RUN_CAP=3", "scatter_zoo", 6, True),
                 # test_lds_poison_bitexact (POISON_CASES)
                 ("PT_POISON_LDS=1 PT_ROOM_CAP=3", "scene_p1", 8, False),
-                ("PT_POISON_LDS=1 PT_ROOM_CAP=3", "csg_zoo", 6, False)]
+                ("PT_POISON_LDS=1 PT_ROOM_CAP=3", "csg_zoo", 6, False),
+                # test_occlusion_settles_more_children
+                ("PT_OCCLUDE=0", "occlude_box", 3, False)]

@@ -148,6 +148,27 @@ def build(name):
     return globals()[name]()
 
 
+def occlude_box(variant="box"):
+    """Union-only scene for the plane-occluder dark test (tests/test_occlude.py):
+    diffuse, glossy and mirror spheres over a ground plane inside a box of
+    emissive half-spaces 3 from the origin on x and y and 8 on z, so ground
+    entries fall on both sides of the emitters' bound; "emissive_sphere" adds a
+    lit sphere (no bound, no claim), "tilted" tilts the ground (not
+    axis-aligned, no claim)."""
+    diffuse = Material(ColorTexture(0.8), ColorTexture(1))
+    glossy = Material(ColorTexture(0.7), ColorTexture(0.5))
+    mirror = Material(ColorTexture(0.99), ColorTexture(0))
+    sky = Material(ColorTexture(0), ColorTexture(0), ColorTexture((0.5, 0.7, 1.0)))
+    ground = Plane((0.05, 1, 0), 0.7, diffuse) if variant == "tilted" else Plane((0, 1, 0), 0.7, diffuse)
+    objs = [Sphere((-0.8, -0.2, -4), 0.5, diffuse), Sphere((0.8, -0.25, -4), 0.45, glossy),
+            Sphere((0, 0.1, -5), 0.5, mirror), ground]
+    if variant == "emissive_sphere":
+        objs.append(Sphere((0, 1.5, -4.5), 0.3, Material(ColorTexture(0), ColorTexture(0), ColorTexture(3.0))))
+    for n in [(0, 0, -1), (0, 0, 1), (0, -1, 0), (0, 1, 0), (1, 0, 0), (-1, 0, 0)]:
+        objs.append(Plane(n, 8 if n[2] else 3, sky))
+    return union_array(objs)
+
+
 def union_zoo():
     """Union-only scene for the union rule (pt_device.h union_min_ok): an
     emissive box of six inward half-spaces, spheres that overlap, nest and
