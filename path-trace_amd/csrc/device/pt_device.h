@@ -2776,7 +2776,7 @@ __device__ __forceinline__ Attempt2 attempt2_draws(W2 a1, W2 a2, W2 a3, W2 b1, W
         z = z + kR.z;
     }
 #ifndef PT_HEMI_MODE
-#define PT_HEMI_MODE 0 /* A/B on C3 with the bit-plane rounds at 1024 spp: 0 +0.9 % over 1 (round 4: 1 +0.8 % over 0) */
+#define PT_HEMI_MODE 1 /* same-box A/B at 1024 spp on the round-6 kernel: 1 +0.9 % over 0 on C3, C2 +0.4..1.6 % (profiles/round6/ab_hemi_mode_r6.txt; round 5: 0 +0.9 % over 1; round 4: 1 +0.8 % over 0) */
 #endif
 #if PT_HEMI_MODE == 1
     /* dot(n, w) per attempt on scalar n (3 SGPRs rather than 3 splatted pairs) */
