@@ -413,9 +413,13 @@ Generated generate(const SceneImpl &s, int depth, bool rays)
         src << "#ifndef PT_SPHERE_SKIP\n#define PT_SPHERE_SKIP 1\n#endif\n"
             << "#ifndef PT_KATT\n#define PT_KATT 6\n#endif\n";
     /* trees with a Difference and no lane walks (C3): 10 attempts per lane
-     * (+1.1 %, 3 of 3 reps, profiles/round4/ab_katt_c3.txt; 6: -5.4 %) */
+     * (+1.1 %, 3 of 3 reps, profiles/round4/ab_katt_c3.txt; 6: -5.4 %), and the
+     * next chunk's dequeue in flight while a chunk is traced (round 6, on the
+     * final kernel: +0.4 %, 6 of 6 same-box pairs at 1 024 spp,
+     * profiles/round6/ab_dequeue_prefetch_c3.txt; round 4's kernel: -0.5 %) */
     else if (s.lane_walk == 0 && !s.lane_scatter)
-        src << "#ifndef PT_KATT\n#define PT_KATT 10\n#endif\n";
+        src << "#ifndef PT_KATT\n#define PT_KATT 10\n#endif\n"
+            << "#ifndef PT_DEQUEUE_PREFETCH\n#define PT_DEQUEUE_PREFETCH 1\n#endif\n";
     /* ... and are scheduled by the iterative max-occupancy strategy (same-box
      * A/B at 1 024 spp: C3 +0.3 %, 4 of 4 reps; C5 -2.6 %, C2 -0.4 %,
      * profiles/round5/ab_sched_maxocc.txt); not when the PT_JIT_OPTIONS hook
