@@ -75,3 +75,19 @@ def test_emis_finite_is_decided_by_the_bound(built):
     assert key(SKIES["inf"]()) != finite
     assert key(ColorTexture((float("nan"), 1.0, 1.0))) == key(SKIES["inf"]())
     assert key(SKIES["overflow"]()) != key(MultiplyTexture((2.0, 1.0, 1.0), ColorTexture((1e20, 0.7, 1.0))))
+
+
+def test_emis_finite_scans_image_texels(built):
+    """an image-mapped emission is bounded by its texels (the lookups are
+    bounds-checked): a finite image keeps the skip, one infinite texel drops it,
+    and a LogTexture over that image (its filter maps +inf to +inf) too"""
+    from pathtrace.scene import Image, ImageTexture, LogTexture, SphericalCoordinatesSkymapTexture
+    img = np.full((8, 16, 4), 0.5, np.float32)
+    bad = img.copy()
+    bad[3, 5, 1] = np.inf
+    key = lambda tex: pt.DeviceScene(sky_scene(tex)).kernel_key(DEPTH)  # noqa: E731
+    fin = key(SphericalCoordinatesSkymapTexture(ImageTexture(Image(img))))
+    inf = key(SphericalCoordinatesSkymapTexture(ImageTexture(Image(bad))))
+    assert fin != inf
+    assert key(SphericalCoordinatesSkymapTexture(ImageTexture(Image(img * 2)))) == fin
+    assert key(LogTexture(ImageTexture(Image(bad)))) != key(LogTexture(ImageTexture(Image(img))))
