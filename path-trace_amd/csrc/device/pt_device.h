@@ -1448,6 +1448,23 @@ struct UnionAcc
         found |= cand;
     }
 };
+/* Opposite unit-normal planes of one axis taken as a pair (PT_PLANE_PAIR):
+ * with the origin outside both solids (num <= -eps^2, burst-uniform), a lane
+ * moving along -e_k enters only the n_k = +1 plane and leaves the other, whose
+ * span [-max_value, t < 0] (or a dead one) is no candidate, no tie, no NaN for
+ * the union rule -- so one quotient per lane, of the plane it enters, gives
+ * the same accumulation as both.  Compact<Pln>::run parks the first such
+ * plane of each (axis, side) here; compact_first_hit evaluates the parked
+ * ones once the tree is walked (a pair when both sides are parked). */
+#ifndef PT_PLANE_PAIR
+#define PT_PLANE_PAIR 1
+#endif
+struct PlaneStash
+{
+    float num[3][2];
+    int mat[3][2];
+    int has[3][2];
+};
 template <class N>
 struct Compact
 {
@@ -1457,8 +1474,8 @@ template <int P, int O, int M>
 struct Compact<Sph<P, O, M>>
 {
     static constexpr bool OK = P < 64;
-    __device__ static __forceinline__ void run(UnionAcc &, u64 &m, const typename Sph<P, O, M>::Ctx &c, const Ray &q,
-                                               const Env &)
+    __device__ static __forceinline__ void run(UnionAcc &, u64 &m, PlaneStash &,
+                                               const typename Sph<P, O, M>::Ctx &c, const Ray &q, const Env &)
     {
         const float b = dot(c.omc, q.d);
         const float disc = b * b - q.a * c.c;
@@ -1475,9 +1492,18 @@ template <int P, int O, int M, int AX, int U>
 struct Compact<Pln<P, O, M, AX, U>>
 {
     static constexpr bool OK = true;
-    __device__ static __forceinline__ void run(UnionAcc &acc, u64 &, const typename Pln<P, O, M, AX, U>::Ctx &c,
-                                               const Ray &q, const Env &e)
+    __device__ static __forceinline__ void run(UnionAcc &acc, u64 &, PlaneStash &st,
+                                               const typename Pln<P, O, M, AX, U>::Ctx &c, const Ray &q, const Env &e)
     {
+#if defined(PT_AXIS_SHARE) && PT_PLANE_PAIR
+        if constexpr (U != 0 && AX >= 0) {
+            constexpr int k = AX >> 1, side = AX & 1;
+            if (c.num <= -(EPS * EPS) && !st.has[k][side]) {
+                st.num[k][side] = c.num, st.mat[k][side] = M, st.has[k][side] = 1;
+                return;
+            }
+        }
+#endif
         typename Pln<P, O, M, AX, U>::St s;
         Pln<P, O, M, AX, U>::init(s, c, q, e);
         acc.add(s.live, s.t0, s.t1, M);
@@ -1488,11 +1514,11 @@ template <class A, class B>
 struct Compact<Uni<A, B>>
 {
     static constexpr bool OK = Compact<A>::OK && Compact<B>::OK;
-    __device__ static __forceinline__ void run(UnionAcc &acc, u64 &m, const typename Uni<A, B>::Ctx &c, const Ray &q,
-                                               const Env &e)
+    __device__ static __forceinline__ void run(UnionAcc &acc, u64 &m, PlaneStash &st, const typename Uni<A, B>::Ctx &c,
+                                               const Ray &q, const Env &e)
     {
-        Compact<A>::run(acc, m, c.a, q, e);
-        Compact<B>::run(acc, m, c.b, q, e);
+        Compact<A>::run(acc, m, st, c.a, q, e);
+        Compact<B>::run(acc, m, st, c.b, q, e);
     }
     __device__ static __forceinline__ void fill(float4 *tab, int *mt, const typename Uni<A, B>::Ctx &c)
     {
@@ -1508,7 +1534,44 @@ __device__ __forceinline__ int compact_first_hit(const typename R::Ctx &ctx, con
 {
     UnionAcc acc;
     u64 m = 0ull;
-    Compact<R>::run(acc, m, ctx, q, e);
+    PlaneStash st;
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        st.has[k][0] = st.has[k][1] = 0;
+    Compact<R>::run(acc, m, st, ctx, q, e);
+#if defined(PT_AXIS_SHARE) && PT_PLANE_PAIR
+    /* the parked unit planes: Pln::init's UNIT arithmetic on the plane each
+     * lane enters (n_k = +1 when d_k < 0), or on each parked plane alone */
+    auto unit_plane = [&](int k, int side, float num, int mat) {
+        const float dk = k == 0 ? q.d.x : k == 1 ? q.d.y : q.d.z;
+        const float div = side ? -dk : dk; /* n_k d_k, n_k = +-1 exactly */
+        const bool small = __builtin_fabsf(div) < EPS * EPS;
+        const float q0 = div_core(num, q.rk[k]);
+        float t = side ? -q0 : q0;
+        const bool bad = !small && !(q.rkok[k] && num_ok(num));
+        if (wave_any(bad)) {
+            if (bad)
+                t = num / div;
+        }
+        const bool deg = small || __builtin_fabsf(t) >= MAXV;
+        const bool neg = div < 0.0f;
+        acc.add((!deg || __builtin_fabsf(num) < EPS * EPS) ? 1 : 0, (!deg && neg) ? t : -MAXV,
+                (!deg && !neg) ? t : MAXV, mat);
+    };
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        if (st.has[k][0] && st.has[k][1]) {
+            const float dk = k == 0 ? q.d.x : k == 1 ? q.d.y : q.d.z;
+            const int side = dk < 0.0f ? 0 : 1;
+            unit_plane(k, side, side ? st.num[k][1] : st.num[k][0], side ? st.mat[k][1] : st.mat[k][0]);
+        } else {
+            if (st.has[k][0])
+                unit_plane(k, 0, st.num[k][0], st.mat[k][0]);
+            if (st.has[k][1])
+                unit_plane(k, 1, st.num[k][1], st.mat[k][1]);
+        }
+    }
+#endif
     while (wave_any(m != 0ull)) {
         if (m != 0ull) {
             const int k = __builtin_ctzll(m);
