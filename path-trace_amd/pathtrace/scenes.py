@@ -218,12 +218,15 @@ CONFIGS: Dict[str, Config] = {
                  fast_spine=True),
     # C5 at 2 workgroups per CU: its 14-primitive tree spills 1032 VGPRs at the
     # default cap of 128 (119 -> 277 Msamples/s on one MI355X, round 2).  Its
-    # glass-ball trees have no scatter loop: lanes walk them with 2 register
+    # glass-ball trees have no scatter loop: lanes walk them with register
     # frames instead of the wave (bench-like subset at 256 spp 685 -> 2330
-    # Msamples/s, glass disk 65 -> 708; 3 frames 2311, 4 frames 2164)
+    # Msamples/s, glass disk 65 -> 708; 3 frames 2311, 4 frames 2164).  Since
+    # the zero-weight skip (round 6) a sky hit needs no frame for its mirror
+    # child, and one frame is best: 19.09 -> 19.36 G on the bench subset
+    # (2 frames; 3: 18.53; profiles/round6/ab_lane_walk_c5_r6.txt)
     "C5": Config("C5", 3840, 2160, 8192, 16, scene_c5, gpus=8,
                  note="demo world + test.hdr spherical env + sky01 skybox", wg_per_cu=2, fast_spine=True,
-                 lane_walk=2),
+                 lane_walk=1),
 }
 
 
